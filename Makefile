@@ -1,0 +1,55 @@
+# Build everything in-tree (the built files travel to the GPU box with the gpurun snapshot).
+#   make            -> raytracingc_amd/_lib/librtc.so, raytracingc_amd/_lib/rtc (CLI), oracle/liboracle.so,
+#                      oracle/_ref/rtc_ref (only when /root/reference is present)
+# Device code: gfx950 only, -ffp-contract=off, no fast-math.
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CC       ?= gcc
+ARCH     ?= gfx950
+BUILD    := build
+LIBDIR   := raytracingc_amd/_lib
+CSRC     := raytracingc_amd/csrc
+REF      ?= /root/reference
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall
+CFLAGS   := -std=gnu11 -O2 -fPIC -ffp-contract=off -Wall -Wextra
+
+LIB      := $(LIBDIR)/librtc.so
+CLI      := $(LIBDIR)/rtc
+ORACLE   := oracle/liboracle.so
+REFBIN   := oracle/_ref/rtc_ref
+
+all: $(LIB) $(CLI) $(ORACLE) ref
+
+$(BUILD):
+	mkdir -p $(BUILD) $(LIBDIR) oracle/_ref
+
+$(BUILD)/scene_build.o: $(CSRC)/scene_build.c $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/rtc_render.o $(BUILD)/scene_build.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so
+
+$(BUILD)/rtc_main.o: $(CSRC)/rtc_main.c include/rtc.h | $(BUILD)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(CLI): $(BUILD)/rtc_main.o $(LIB)
+	$(CC) $< -o $@ -L$(LIBDIR) -lrtc -Wl,-rpath,'$$ORIGIN' -lm
+
+# CPU restatement (test infrastructure + timed CPU baseline); gcc, SSE2, no FMA contraction
+$(ORACLE): oracle/rtc_oracle.c include/rtc.h | $(BUILD)
+	$(CC) -std=gnu11 -O3 -fPIC -shared -ffp-contract=off -Wall $< -o $@ -lm -lpthread
+
+# The reference's own sources, built where they lie (no copy), deterministic variant (oracle/ref_unity.c)
+ref: | $(BUILD)
+	@if [ -d $(REF) ]; then \
+	  $(CC) -std=gnu99 -O3 -w -I$(REF) oracle/ref_unity.c -o $(REFBIN) -lm -lpthread && echo "built $(REFBIN)"; \
+	else echo "no $(REF): keeping prebuilt $(REFBIN) if any"; fi
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(CLI) $(ORACLE) $(REFBIN)
+
+.PHONY: all ref clean

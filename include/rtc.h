@@ -1,0 +1,145 @@
+/*
+ * rtc.h -- C ABI of the MI355X-native render path (librtc.so).
+ *
+ * This is the drop-in boundary for the reference's render seam, main.c:263-304 (the pthread fan-out of
+ * rowThread, main.c:81-104, over calcColor raytracing.c:262-296).  The reference has no plugin or FFI API;
+ * its only "interface" for this path is that seam plus the scene-build / output functions either side
+ * of it, so the entry points below are what a maintainer binds in place of that region.
+ *
+ * Plain C: plain pointers and sizes, no torch or HIP types.  All structs keep the reference's byte
+ * layouts (raytracing.h:7-69, moremath.h:10-13) so host arrays produced by the reference's own loaders
+ * pass through unconverted.
+ *
+ * Error convention: 0 = OK; a negative value is either -(hipError_t) (|v| < 10000) or one of the RTC_E*
+ * codes below.  Nothing here calls exit(); rtc_last_error() returns a message for the calling thread.
+ */
+#ifndef RTC_H
+#define RTC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference types (identical layouts; sizes are static_assert-ed in the implementation) ------------ */
+typedef unsigned char uint8;                                                   /* moremath.h:6 */
+typedef struct vec3 { float x, y, z; } vec3;                                   /* moremath.h:10-13, 12 B */
+typedef struct Scene {                                                         /* raytracing.h:7-11, 56 B */
+    vec3 normalizedSunDirection, skyColorHorizon, skyColorZenith, groundColor;
+    float sunFocus, sunIntensity;
+} Scene;
+typedef struct Color { uint8 r, g, b; } Color;                                 /* raytracing.h:15-18, 3 B */
+typedef struct Material { vec3 color; float emissionStrength; float smoothness; } Material; /* :25-30, 20 B */
+typedef struct Sphere { vec3 pos; float r; Material mat; } Sphere;             /* raytracing.h:34-39, 36 B */
+typedef struct Triangle { vec3 posA, posB, posC, normal; Material mat; } Triangle; /* :41-45, 68 B */
+typedef struct Ray { vec3 pos; vec3 dir; } Ray;                                /* raytracing.h:64-68, 24 B */
+
+/* ---- render description ---------------------------------------------------------------------------- */
+/* Camera: origin plus the basis main.c:252-255 computes, and fov (main.c:116). */
+typedef struct RtcCamera { vec3 origin, ex, ey, ez; float fov; } RtcCamera;   /* 52 B */
+
+/* Which pixels and how.  width/height/maxBounce = main.c:10-12; spp = accumulationCount (scene.h:26);
+ * trianglesOnly = main.c:113,241.  Rows rendered: y = rowStart + k*rowStride for k = 0..ceil(..)-1, the
+ * reference's row interleave (main.c:84) lifted to devices/ranks.  rowStride = 1, rowStart = 0 renders the
+ * whole frame. */
+typedef struct RtcRenderDesc {
+    int width, height;
+    int spp;
+    int maxBounce;
+    int trianglesOnly;
+    int rowStart, rowStride;
+    int flags;                 /* RTC_F_* */
+} RtcRenderDesc;
+
+#define RTC_F_HOIST_PRIMARY 0x1  /* bit-exact: trace each pixel's primary ray once; default off */
+
+typedef struct RtcStats {
+    double renderMs;             /* device time of the render kernel(s), HIP events */
+    double totalMs;              /* wall time of the whole rtc_render call incl. uploads / D2H */
+    unsigned long long segments; /* closest-hit queries traced (calculateRayCollision calls) */
+    unsigned long long samples;  /* camera samples = pixels * spp */
+} RtcStats;
+
+/* ---- error codes ----------------------------------------------------------------------------------- */
+#define RTC_OK 0
+#define RTC_EINVAL (-10001)
+#define RTC_ENODEV (-10002)
+#define RTC_EIO (-10003)
+#define RTC_ENOMEM (-10004)
+#define RTC_EFORMAT (-10005)
+
+const char *rtc_last_error(void);
+const char *rtc_version(void);
+int rtc_device_count(int *count);
+
+/* ---- scene build (host; restates objloader.c:340-551 + raytracing.c:19-147) ------------------------ */
+/* loadOBJTriangles (raytracing.c:100-147): OBJ/MTL -> Triangle[] with the x,y negation.  On failure
+ * returns RTC_EIO (the reference exits 42, raytracing.c:106-110; the CLI driver keeps that). *outTris is
+ * malloc'd; free with rtc_free. */
+int rtc_load_obj(const char *path, Triangle **outTris, int *outCount);
+/* parseTriangleFile (raytracing.c:76-98) incl. cleanFile (:47-74).  Writes "<path>.parsed" beside the
+ * input exactly like the reference.  Missing file -> RTC_EIO with count 0 (the reference silently keeps 0). */
+int rtc_parse_triangle_file(const char *path, Triangle **outTris, int *outCount);
+void rtc_free(void *p);
+/* The default scene's sphere list (scene.h:17-19) and sky/sun (main.c:14,21-28), sun normalised as main.c:247. */
+int rtc_default_spheres(const Sphere **outSpheres, int *outCount);
+int rtc_default_scene(Scene *outScene);
+int rtc_scene_set_sun(Scene *scene, vec3 sunDirection);
+/* main.c:252-255 */
+int rtc_camera_basis(vec3 origin, vec3 lookingAt, float fov, RtcCamera *outCam);
+/* 24-bit BMP, byte-identical to stbi_write_bmp (stbi_image_write.h:492-529) */
+int rtc_write_bmp(const char *path, int width, int height, const Color *image);
+/* vec3ToColor / floatToUint (raytracing.c:11-15, moremath.c:25-30) on a host float3 buffer */
+int rtc_quantize(const float *accum, size_t pixels, Color *out);
+
+/* ---- render: host buffers (the seam main.c:263-304) ------------------------------------------------ */
+/* Uploads the scene to HBM, renders the rows selected by d (normally the full frame) on `device`
+ * (-1 = current), writes Color rows (row-major, y = 0 top; a partial row set is written compactly in
+ * row order) and optionally the pre-quantisation float3 accumulator.  Inputs are borrowed for the call. */
+int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+               const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int device,
+               Color *outImage, float *outAccum, RtcStats *stats);
+
+/* Single-process multi-GPU variant of rtc_render: devices 0..numDevices-1 each render the rows
+ * y = g + k*numDevices (the reference's row interleave, main.c:84, lifted to GPUs), concurrently; the
+ * parts are copied back and re-interleaved.  Output is bit-identical to numDevices = 1 (the seed is the
+ * absolute pixel index, main.c:95).  stats->renderMs = slowest device. */
+int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                     const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
+                     Color *outImage, float *outAccum, RtcStats *stats);
+
+/* ---- render: device-resident (used by the multi-GPU host and bench) -------------------------------- */
+typedef struct RtcDeviceScene RtcDeviceScene;
+int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                     int device, RtcDeviceScene **out);
+int rtc_scene_release(RtcDeviceScene *s);
+/* Number of rows d selects: ceil((height - rowStart) / rowStride), 0 if none. */
+int rtc_rows_selected(const RtcRenderDesc *d);
+/* Asynchronous on `stream` (a hipStream_t, NULL = default stream).  dColors: device buffer of
+ * rows_selected*width*3 bytes; dAccum: nullable device float buffer rows_selected*width*3; dSegments:
+ * nullable device u64[2] the kernel atomically adds to: [0] calculateRayCollision calls (the reference's
+ * segment count), [1] closest-hit queries actually traced (smaller with RTC_F_HOIST_PRIMARY). */
+int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
+                          const RtcRenderDesc *d, void *dColors, float *dAccum,
+                          unsigned long long *dSegments, void *stream);
+/* Re-assemble a row-interleaved gather: dCompact holds `parts` blocks of rowsPerPart*width*3 bytes, block
+ * g holding rows y = g + k*parts; dOut receives the height*width*3 frame.  Asynchronous on `stream`. */
+int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,
+                           void *dOut, void *stream);
+
+/* ---- device probes: run single reference functions on the GPU for known-answer tests --------------- */
+/* Each copies inputs to the current device, runs one kernel of the same device code the renderer uses,
+ * and copies results back (synchronous). */
+int rtc_probe_ray_triangle(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst);   /* raytracing.c:186 */
+int rtc_probe_ray_sphere(const Ray *rays, const Sphere *spheres, size_t n, int *didHit, float *dst,
+                         vec3 *normal);                                                                 /* raytracing.c:162 */
+int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *out);                  /* raytracing.c:151 */
+int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
+                     vec3 *direction);                                                                  /* moremath.c:89-108 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTC_H */

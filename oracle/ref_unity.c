@@ -1,0 +1,277 @@
+/*
+ * oracle/ref_unity.c -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as the product).
+ *
+ * Builds the *reference's own sources* (/root/reference, read-only, included by path, never copied)
+ * into a deterministic oracle binary `oracle/_ref/rtc_ref`, following SURVEY.md F4 / Appendix B:
+ *
+ *   (1) one unity translation unit (moremath.c + raytracing.c + objloader.c + main.c), so that the
+ *       per-pixel seed store `rngState = x + y*width` (main.c:95) reaches RandomValue (moremath.c:91);
+ *   (2) rngState made thread-local (scene.h:35 declares it `static unsigned int rngState;` -- the macro
+ *       below turns that line into a declaration of a static accessor returning a __thread slot);
+ *   (3) accumulationCount (scene.h:26, hard-coded 4000) made settable at run time: `const` is defined
+ *       away for the reference TUs only (system headers are included first, un-modified), so the
+ *       `static int const accumulationCount = 100 * 40;` line becomes a plain static int we overwrite;
+ *   (4) a float capture hook on vec3ToColor (raytracing.c:11) used by rowThread (main.c:100), giving the
+ *       pre-quantisation framebuffer;
+ *   (5) KAT entry points that call the reference functions themselves (RandomValue, rayTriangle,
+ *       raySphere, getEnvironmentLight, calcColor, loaders) on inputs read from binary files.
+ *
+ * Behaviour of the render is otherwise exactly the reference's (same flags, same BMP, 12 row-interleaved
+ * pthreads main.c:43,84).  The wrapper main parses its own leading options and forwards the rest to the
+ * reference main (renamed rtc_ref_main).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdarg.h>
+#include <string.h>
+#include <math.h>
+#include <assert.h>
+#include <stddef.h>
+#include <libgen.h>
+#include <pthread.h>
+#include <sys/types.h>
+
+/* (2) thread-local RNG state: scene.h:35 `static unsigned int rngState;` becomes
+ *     `static unsigned int (*rtc_ref_rng());` -- a redeclaration of the accessor below. */
+static __thread unsigned int rtc_ref_rng_tls;
+static unsigned int *rtc_ref_rng(void) { return &rtc_ref_rng_tls; }
+#define rngState (*rtc_ref_rng())
+
+/* float capture (4): declared before main.c, defined after it */
+static void rtc_ref_capture(int x, int y, float r, float g, float b);
+
+/* (3) make accumulationCount writable */
+#define const
+#define main rtc_ref_main
+#include "moremath.c"
+#include "raytracing.c"
+#include "objloader.c"
+#define vec3ToColor(v) (rtc_ref_capture(x, y, (v).x, (v).y, (v).z), vec3ToColor(v))
+#include "main.c"
+#undef vec3ToColor
+#undef main
+#undef const
+
+/* ------------------------------------------------------------------------------------------------ */
+static float *g_fb = NULL;
+static int g_fb_w = 0, g_fb_h = 0;
+static pthread_mutex_t g_fb_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void rtc_ref_capture(int x, int y, float r, float g, float b)
+{
+    if (g_fb == NULL) {
+        pthread_mutex_lock(&g_fb_mu);
+        if (g_fb == NULL) {
+            float *p = calloc((size_t)width * (size_t)height * 3, sizeof(float));
+            g_fb_w = width;
+            g_fb_h = height;
+            __atomic_store_n(&g_fb, p, __ATOMIC_RELEASE);
+        }
+        pthread_mutex_unlock(&g_fb_mu);
+    }
+    size_t i = ((size_t)x + (size_t)y * (size_t)g_fb_w) * 3;
+    g_fb[i] = r;
+    g_fb[i + 1] = g;
+    g_fb[i + 2] = b;
+}
+
+static void die(const char *msg)
+{
+    fprintf(stderr, "rtc_ref: %s\n", msg);
+    exit(3);
+}
+
+static void *read_all(const char *path, size_t *n)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        die("cannot open KAT input");
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    void *buf = malloc(sz > 0 ? (size_t)sz : 1);
+    if (sz > 0 && fread(buf, 1, (size_t)sz, f) != (size_t)sz)
+        die("short read");
+    fclose(f);
+    *n = (size_t)sz;
+    return buf;
+}
+
+static void write_all(const char *path, const void *buf, size_t n)
+{
+    FILE *f = fopen(path, "wb");
+    if (!f)
+        die("cannot open KAT output");
+    if (n && fwrite(buf, 1, n, f) != n)
+        die("short write");
+    fclose(f);
+}
+
+/* Triangle dump: int32 count, int32 trianglesOnly, then count * 68-byte Triangle (raytracing.h:41-45). */
+static void dump_tris(const char *path, int trianglesOnlyFlag)
+{
+    FILE *f = fopen(path, "wb");
+    if (!f)
+        die("cannot open triangle dump");
+    fwrite(&triangleCount, 4, 1, f);
+    fwrite(&trianglesOnlyFlag, 4, 1, f);
+    if (triangleCount > 0)
+        fwrite(triangles, sizeof(Triangle), (size_t)triangleCount, f);
+    fclose(f);
+}
+
+static void load_scene_mode(const char *mode, int *trianglesOnlyOut)
+{
+    if (strcmp(mode, "default") == 0) {
+        parseTriangleFile("triangles.txt");
+        *trianglesOnlyOut = 0;
+    } else {
+        loadOBJTriangles(mode);
+        *trianglesOnlyOut = 1;
+    }
+}
+
+typedef struct { Ray ray; Triangle t; } KatTriIn;                     /* 92 B */
+typedef struct { int didHit; float dst; vec3 normal; } KatTriOut;     /* 20 B */
+typedef struct { Ray ray; vec3 c; float r; } KatSphIn;                /* 40 B */
+typedef struct { int didHit; float dst; vec3 hitPoint; vec3 normal; } KatSphOut; /* 32 B */
+typedef struct { Ray ray; Scene s; } KatEnvIn;                        /* 80 B */
+typedef struct { Ray ray; unsigned int seed; int maxBounce; } KatCalcIn; /* 32 B */
+typedef struct { vec3 color; unsigned int seedAfter; } KatCalcOut;      /* 16 B */
+
+typedef struct { int argc; char **argv; int rc; } RefMainArgs;
+static void *ref_main_thread(void *p)
+{
+    RefMainArgs *m = p;
+    m->rc = rtc_ref_main(m->argc, m->argv);
+    return NULL;
+}
+
+int main(int argc, char **argv)
+{
+    int spp = 4000;
+    const char *dumpFloat = NULL;
+    int a = 1;
+    /* wrapper options come first; everything after is forwarded to the reference main */
+    while (a < argc) {
+        if (strcmp(argv[a], "--spp") == 0 && a + 1 < argc) {
+            spp = atoi(argv[a + 1]);
+            a += 2;
+        } else if (strcmp(argv[a], "--dump-float") == 0 && a + 1 < argc) {
+            dumpFloat = argv[a + 1];
+            a += 2;
+        } else if (strcmp(argv[a], "--kat-rng") == 0 && a + 3 < argc) {
+            /* --kat-rng <seed> <count> <out>: count x {RandomValue} then count x {normal} then
+             * count x {RandomDiretion}, each restarted from seed (moremath.c:89-108) */
+            unsigned int seed = (unsigned int)strtoul(argv[a + 1], NULL, 0);
+            int n = atoi(argv[a + 2]);
+            float *out = malloc(sizeof(float) * (size_t)n * 5);
+            rngState = seed;
+            for (int i = 0; i < n; ++i)
+                out[i] = RandomValue();
+            rngState = seed;
+            for (int i = 0; i < n; ++i)
+                out[n + i] = RandomValueNormalDistrubtion();
+            rngState = seed;
+            for (int i = 0; i < n; ++i) {
+                vec3 d = RandomDiretion();
+                out[2 * n + 3 * i] = d.x;
+                out[2 * n + 3 * i + 1] = d.y;
+                out[2 * n + 3 * i + 2] = d.z;
+            }
+            write_all(argv[a + 3], out, sizeof(float) * (size_t)n * 5);
+            return 0;
+        } else if (strcmp(argv[a], "--kat-tri") == 0 && a + 2 < argc) {
+            size_t nb;
+            KatTriIn *in = read_all(argv[a + 1], &nb);
+            size_t n = nb / sizeof(KatTriIn);
+            KatTriOut *out = calloc(n ? n : 1, sizeof(KatTriOut));
+            for (size_t i = 0; i < n; ++i) {
+                HitInfo h = rayTriangle(in[i].ray, in[i].t);
+                out[i].didHit = h.didHit;
+                out[i].dst = h.dst;
+                out[i].normal = h.normal;
+            }
+            write_all(argv[a + 2], out, n * sizeof(KatTriOut));
+            return 0;
+        } else if (strcmp(argv[a], "--kat-sphere") == 0 && a + 2 < argc) {
+            size_t nb;
+            KatSphIn *in = read_all(argv[a + 1], &nb);
+            size_t n = nb / sizeof(KatSphIn);
+            KatSphOut *out = calloc(n ? n : 1, sizeof(KatSphOut));
+            for (size_t i = 0; i < n; ++i) {
+                HitInfo h = raySphere(in[i].ray, in[i].c, in[i].r);
+                out[i].didHit = h.didHit;
+                out[i].dst = h.dst;
+                out[i].hitPoint = h.hitPoint;
+                out[i].normal = h.normal;
+            }
+            write_all(argv[a + 2], out, n * sizeof(KatSphOut));
+            return 0;
+        } else if (strcmp(argv[a], "--kat-env") == 0 && a + 2 < argc) {
+            size_t nb;
+            KatEnvIn *in = read_all(argv[a + 1], &nb);
+            size_t n = nb / sizeof(KatEnvIn);
+            vec3 *out = calloc(n ? n : 1, sizeof(vec3));
+            for (size_t i = 0; i < n; ++i)
+                out[i] = getEnvironmentLight(in[i].ray, in[i].s);
+            write_all(argv[a + 2], out, n * sizeof(vec3));
+            return 0;
+        } else if (strcmp(argv[a], "--kat-calc") == 0 && a + 3 < argc) {
+            /* --kat-calc <mode: default|path.obj> <in> <out>: calcColor (raytracing.c:262) per record */
+            int tonly;
+            load_scene_mode(argv[a + 1], &tonly);
+            /* main() normally fills the sun before rendering (main.c:247-250) */
+            scene.normalizedSunDirection = normalized(sunDirection);
+            size_t nb;
+            KatCalcIn *in = read_all(argv[a + 2], &nb);
+            size_t n = nb / sizeof(KatCalcIn);
+            KatCalcOut *out = calloc(n ? n : 1, sizeof(KatCalcOut));
+            for (size_t i = 0; i < n; ++i) {
+                rngState = in[i].seed;
+                out[i].color = calcColor(in[i].ray, tonly, in[i].maxBounce, scene);
+                out[i].seedAfter = rngState;
+            }
+            write_all(argv[a + 3], out, n * sizeof(KatCalcOut));
+            return 0;
+        } else if (strcmp(argv[a], "--dump-tris") == 0 && a + 2 < argc) {
+            /* --dump-tris <mode: default|path.obj> <out> */
+            int tonly;
+            load_scene_mode(argv[a + 1], &tonly);
+            dump_tris(argv[a + 2], tonly);
+            return 0;
+        } else {
+            break;
+        }
+    }
+    accumulationCount = spp;
+
+    int fargc = argc - a + 1;
+    char **fargv = malloc(sizeof(char *) * (size_t)(fargc + 1));
+    fargv[0] = argv[0];
+    for (int i = a; i < argc; ++i)
+        fargv[i - a + 1] = argv[i];
+    fargv[fargc] = NULL;
+    /* the reference keeps the framebuffer in a stack VLA (main.c:246): run it on a thread
+     * with a 1 GiB stack so 4K frames work without `ulimit -s unlimited` */
+    RefMainArgs ma = {fargc, fargv, 0};
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    pthread_attr_setstacksize(&attr, (size_t)1 << 30);
+    pthread_t th;
+    if (pthread_create(&th, &attr, ref_main_thread, &ma) != 0)
+        die("pthread_create failed");
+    pthread_join(th, NULL);
+    int rc = ma.rc;
+
+    if (dumpFloat != NULL && g_fb != NULL) {
+        FILE *f = fopen(dumpFloat, "wb");
+        if (!f)
+            die("cannot open float dump");
+        fwrite(&g_fb_w, 4, 1, f);
+        fwrite(&g_fb_h, 4, 1, f);
+        fwrite(g_fb, sizeof(float), (size_t)g_fb_w * (size_t)g_fb_h * 3, f);
+        fclose(f);
+    }
+    return rc;
+}

@@ -1,0 +1,276 @@
+"""raytracingc_amd -- MI355X-native render path of Atsuyo64/RayTracingC.
+
+The product is librtc.so (HIP kernels for gfx950 behind the C ABI in include/rtc.h).  This package is the
+thin host mirror of the reference's interface for that path, with the reference's names:
+
+  scene build   loadOBJTriangles (raytracing.c:100), parseTriangleFile (raytracing.c:76),
+                DEFAULT_SPHERES (scene.h:17-19), default_scene (main.c:14,21-28), camera_basis (main.c:252-255)
+  render seam   render (main.c:263-304 -> one rtc_render call), render_multi (one process, many GPUs),
+                DeviceScene.render_rows_async (device-resident, used by the multi-rank host and bench.py)
+  output        vec3ToColor (raytracing.c:11), write_bmp (stbi_write_bmp, main.c:305)
+  device probes rayTriangle, raySphere, getEnvironmentLight, RandomValue / RandomValueNormalDistrubtion /
+                RandomDiretion -- the renderer's own device functions run on the GPU, for known-answer tests.
+
+There is no CPU fallback: every render call goes to the GPU and raises if librtc.so or the GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._abi import (  # noqa: F401
+    CLI_PATH,
+    LIB_PATH,
+    RAY_DT,
+    RTC_F_HOIST_PRIMARY,
+    SCENE_DT,
+    SPHERE_DT,
+    TRIANGLE_DT,
+    VEC3_DT,
+    EXPORTS,
+    Ray,
+    RtcCamera,
+    RtcError,
+    RtcRenderDesc,
+    RtcStats,
+    Scene,
+    Vec3,
+    check,
+    lib,
+)
+from ._abi import _ptr
+
+__all__ = [
+    "loadOBJTriangles", "parseTriangleFile", "default_spheres", "default_scene", "camera_basis", "RenderConfig",
+    "render", "render_multi", "DeviceScene", "vec3ToColor", "write_bmp", "rayTriangle", "raySphere",
+    "getEnvironmentLight", "random_sequences", "device_count", "lib", "TRIANGLE_DT", "SPHERE_DT", "RAY_DT",
+    "SCENE_DT", "RtcError",
+]
+
+# main.c:114-116 (camera) and main.c:10-12 (frame) defaults
+DEFAULT_ORIGIN = (-4.75, -1.5, -4.75)
+DEFAULT_LOOKING_AT = (0.9, -1.2, 1.0)
+DEFAULT_FOV = 1.0
+DEFAULT_SUN = (-30.0, -85.0, 100.0)
+
+
+def _take_tris(p: C.c_void_p, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=TRIANGLE_DT)
+    if n:
+        C.memmove(out.ctypes.data, p.value, n * TRIANGLE_DT.itemsize)
+    lib().rtc_free(p)
+    return out
+
+
+def loadOBJTriangles(path: str) -> np.ndarray:
+    """raytracing.c:100-147 (+ objloader.c): OBJ/MTL -> Triangle[] (x, y negated).  Raises on failure
+    (the reference exits 42)."""
+    p, n = C.c_void_p(), C.c_int()
+    check(lib().rtc_load_obj(path.encode(), C.byref(p), C.byref(n)), "rtc_load_obj")
+    return _take_tris(p, n.value)
+
+
+def parseTriangleFile(path: str) -> np.ndarray:
+    """raytracing.c:76-98: triangles.txt -> Triangle[] with counter-clockwise normals."""
+    p, n = C.c_void_p(), C.c_int()
+    check(lib().rtc_parse_triangle_file(path.encode(), C.byref(p), C.byref(n)), "rtc_parse_triangle_file")
+    return _take_tris(p, n.value)
+
+
+def default_spheres() -> np.ndarray:
+    """scene.h:17-19: the single default-mode sphere."""
+    p, n = C.c_void_p(), C.c_int()
+    check(lib().rtc_default_spheres(C.byref(p), C.byref(n)), "rtc_default_spheres")
+    out = np.empty(n.value, dtype=SPHERE_DT)
+    C.memmove(out.ctypes.data, p.value, n.value * SPHERE_DT.itemsize)
+    return out
+
+
+def default_scene(sun=DEFAULT_SUN, ground=None, horizon=None, zenith=None, focus=None, intensity=None) -> Scene:
+    """main.c:14,21-28 with the CLI overrides of main.c:185-224; the sun is normalised as main.c:247."""
+    s = Scene()
+    check(lib().rtc_default_scene(C.byref(s)), "rtc_default_scene")
+    if ground is not None:
+        s.groundColor = Vec3(*ground)
+    if horizon is not None:
+        s.skyColorHorizon = Vec3(*horizon)
+    if zenith is not None:
+        s.skyColorZenith = Vec3(*zenith)
+    if focus is not None:
+        s.sunFocus = focus
+    if intensity is not None:
+        s.sunIntensity = intensity
+    check(lib().rtc_scene_set_sun(C.byref(s), Vec3(*sun)), "rtc_scene_set_sun")
+    return s
+
+
+def camera_basis(origin=DEFAULT_ORIGIN, looking_at=DEFAULT_LOOKING_AT, fov=DEFAULT_FOV) -> RtcCamera:
+    """main.c:252-255."""
+    cam = RtcCamera()
+    check(lib().rtc_camera_basis(Vec3(*origin), Vec3(*looking_at), C.c_float(fov), C.byref(cam)), "rtc_camera_basis")
+    return cam
+
+
+@dataclass
+class RenderConfig:
+    width: int = 128
+    height: int = 128
+    spp: int = 4000  # scene.h:26
+    max_bounce: int = 10  # main.c:12
+    triangles_only: bool = True
+    hoist: bool = False
+    row_start: int = 0
+    row_stride: int = 1
+
+    def desc(self) -> RtcRenderDesc:
+        return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
+                             self.row_start, self.row_stride, RTC_F_HOIST_PRIMARY if self.hoist else 0)
+
+    def rows(self) -> int:
+        d = self.desc()
+        return lib().rtc_rows_selected(C.byref(d))
+
+
+def _arr(a, dt):
+    if a is None or len(a) == 0:
+        return None, 0
+    a = np.ascontiguousarray(a, dtype=dt)
+    return a, len(a)
+
+
+def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, device: int = -1,
+           want_accum: bool = False):
+    """The render seam (main.c:263-304) on one GPU.  Returns (colors uint8 [rows, W, 3],
+    accum float32 [rows, W, 3] or None, stats dict)."""
+    t, nt = _arr(tris, TRIANGLE_DT)
+    s, ns = _arr(spheres, SPHERE_DT)
+    rows = cfg.rows()
+    colors = np.zeros((rows, cfg.width, 3), np.uint8)
+    accum = np.zeros((rows, cfg.width, 3), np.float32) if want_accum else None
+    st = RtcStats()
+    d = cfg.desc()
+    check(lib().rtc_render(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), device,
+                           _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render")
+    return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
+                           "samples": st.samples}
+
+
+def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, num_devices: int,
+                 want_accum: bool = False):
+    """Full frame, rows interleaved over `num_devices` GPUs of this process (main.c:84 lifted to GPUs)."""
+    t, nt = _arr(tris, TRIANGLE_DT)
+    s, ns = _arr(spheres, SPHERE_DT)
+    colors = np.zeros((cfg.height, cfg.width, 3), np.uint8)
+    accum = np.zeros((cfg.height, cfg.width, 3), np.float32) if want_accum else None
+    st = RtcStats()
+    d = cfg.desc()
+    check(lib().rtc_render_multi(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), num_devices,
+                                 _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render_multi")
+    return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
+                           "samples": st.samples}
+
+
+class DeviceScene:
+    """A scene resident in HBM on one device (rtc_scene_upload).  render_rows_async takes raw device
+    pointers and a hipStream_t (ints), e.g. from torch tensors / torch.cuda streams."""
+
+    def __init__(self, tris, spheres, device: int = -1):
+        t, nt = _arr(tris, TRIANGLE_DT)
+        s, ns = _arr(spheres, SPHERE_DT)
+        h = C.c_void_p()
+        check(lib().rtc_scene_upload(_ptr(t), nt, _ptr(s), ns, device, C.byref(h)), "rtc_scene_upload")
+        self._h = h
+        self.tri_count = nt
+        self.sphere_count = ns
+
+    def render_rows_async(self, scene: Scene, cam: RtcCamera, cfg: RenderConfig, colors_ptr: int,
+                          accum_ptr: int | None = None, segments_ptr: int | None = None, stream: int | None = None):
+        d = cfg.desc()
+        check(lib().rtc_render_rows_async(self._h, C.byref(scene), C.byref(cam), C.byref(d), C.c_void_p(colors_ptr),
+                                          C.c_void_p(accum_ptr) if accum_ptr else None,
+                                          C.c_void_p(segments_ptr) if segments_ptr else None,
+                                          C.c_void_p(stream) if stream else None), "rtc_render_rows_async")
+
+    def close(self):
+        if self._h:
+            lib().rtc_scene_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,
+                       stream: int | None = None):
+    check(lib().rtc_deinterleave_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height,
+                                       C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
+          "rtc_deinterleave_async")
+
+
+def vec3ToColor(accum: np.ndarray) -> np.ndarray:
+    """raytracing.c:11-15 / moremath.c:25-30 on a float3 buffer (host)."""
+    a = np.ascontiguousarray(accum, dtype=np.float32)
+    out = np.empty(a.shape, np.uint8)
+    check(lib().rtc_quantize(_ptr(a), a.size // 3, _ptr(out)), "rtc_quantize")
+    return out
+
+
+def write_bmp(path: str, colors: np.ndarray) -> None:
+    """stbi_write_bmp(path, W, H, 3, image) (main.c:305)."""
+    c = np.ascontiguousarray(colors, dtype=np.uint8)
+    h, w = c.shape[0], c.shape[1]
+    check(lib().rtc_write_bmp(path.encode(), w, h, _ptr(c)), "rtc_write_bmp")
+
+
+def device_count() -> int:
+    n = C.c_int()
+    rc = lib().rtc_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+# ---- device probes (same device code as the renderer) --------------------------------------------------
+def rayTriangle(rays: np.ndarray, tris: np.ndarray):
+    """raytracing.c:186-214 on the GPU, one (ray, triangle) pair per element -> (didHit int32, dst f32)."""
+    r = np.ascontiguousarray(rays, RAY_DT)
+    t = np.ascontiguousarray(tris, TRIANGLE_DT)
+    n = len(r)
+    hit, dst = np.zeros(n, np.int32), np.zeros(n, np.float32)
+    check(lib().rtc_probe_ray_triangle(_ptr(r), _ptr(t), n, _ptr(hit), _ptr(dst)), "rtc_probe_ray_triangle")
+    return hit, dst
+
+
+def raySphere(rays: np.ndarray, spheres: np.ndarray):
+    """raytracing.c:162-184 on the GPU -> (didHit, dst, normal[n,3])."""
+    r = np.ascontiguousarray(rays, RAY_DT)
+    s = np.ascontiguousarray(spheres, SPHERE_DT)
+    n = len(r)
+    hit, dst, nrm = np.zeros(n, np.int32), np.zeros(n, np.float32), np.zeros((n, 3), np.float32)
+    check(lib().rtc_probe_ray_sphere(_ptr(r), _ptr(s), n, _ptr(hit), _ptr(dst), _ptr(nrm)), "rtc_probe_ray_sphere")
+    return hit, dst, nrm
+
+
+def getEnvironmentLight(rays: np.ndarray, scenes: np.ndarray) -> np.ndarray:
+    """raytracing.c:151-160 on the GPU -> float32 [n, 3]."""
+    r = np.ascontiguousarray(rays, RAY_DT)
+    s = np.ascontiguousarray(scenes, SCENE_DT)
+    n = len(r)
+    out = np.zeros((n, 3), np.float32)
+    check(lib().rtc_probe_environment(_ptr(r), _ptr(s), n, _ptr(out)), "rtc_probe_environment")
+    return out
+
+
+def random_sequences(seeds: np.ndarray, draws: int):
+    """moremath.c:89-108 on the GPU: per seed, `draws` x RandomValue, x RandomValueNormalDistrubtion and
+    x RandomDiretion, each sequence restarted from the seed."""
+    sd = np.ascontiguousarray(seeds, np.uint32)
+    n = len(sd)
+    u = np.zeros((n, draws), np.float32)
+    g = np.zeros((n, draws), np.float32)
+    d = np.zeros((n, draws, 3), np.float32)
+    check(lib().rtc_probe_random(_ptr(sd), n, draws, _ptr(u), _ptr(g), _ptr(d)), "rtc_probe_random")
+    return u, g, d

@@ -1,0 +1,159 @@
+/*
+ * rtc_device.h -- device-side restatement of the reference math for gfx950.
+ *
+ * Every function follows the reference expression by expression, with the reference's float<->double
+ * promotions.  The translation unit is compiled with -ffp-contract=off and
+ * without fast-math: a fused multiply-add changes Monte-Carlo paths.  f32 division is the
+ * IEEE one (hipcc default -fhip-fp32-correctly-rounded-divide-sqrt); a double divide rounded to float
+ * equals the f32 IEEE divide (double rounding is innocuous for 53 >= 2*24+2), so `(float)(1./x)` in
+ * the source is `1.f / x` here.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rtcdev {
+
+struct V3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }      /* moremath.c:55-59 */
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }      /* :61-65 */
+__device__ __forceinline__ V3 mul(V3 a, float b) { return V3{a.x * b, a.y * b, a.z * b}; }         /* :67-71 */
+__device__ __forceinline__ V3 mulv(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }     /* :73-77 */
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }     /* :33-36 */
+__device__ __forceinline__ V3 cross(V3 u, V3 v)                                                    /* :43-47 */
+{
+    return V3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+/* length (moremath.c:7-10): sqrt of the f32 sum in double, rounded to float (== correctly rounded sqrtf) */
+__device__ __forceinline__ float length(V3 v) { return (float)__builtin_sqrt((double)(v.x * v.x + v.y * v.y + v.z * v.z)); }
+__device__ __forceinline__ V3 normalized(V3 v) /* :12-17 */
+{
+    float invLen = 1.f / length(v);
+    return V3{v.x * invLen, v.y * invLen, v.z * invLen};
+}
+__device__ __forceinline__ float clamp01(float x) { return x < 0.f ? 0.f : (x > 1.f ? 1.f : x); } /* :38-41 */
+__device__ __forceinline__ float smoothstep(float inf, float sup, float x)                          /* :49-53 */
+{
+    x = clamp01((x - inf) / (sup - inf));
+    return (float)((double)(x * x) * (3.0 - 2.0 * (double)x));
+}
+__device__ __forceinline__ V3 reflect(V3 d, V3 n) { return sub(d, mul(n, 2.f * dot(d, n))); }  /* :79-82; 2*f exact */
+__device__ __forceinline__ V3 lerp(V3 a, V3 b, float t) { return add(mul(a, 1.f - t), mul(b, t)); } /* :84-87 */
+
+/* RandomValue (moremath.c:89-95) on a register-resident per-pixel state */
+__device__ __forceinline__ float random_value(unsigned &s)
+{
+    s = s * 747796405u + 2891336453u;
+    unsigned r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;
+    r = (r >> 22) ^ r;
+    return (float)((double)r / 4294967295.0);
+}
+/* RandomValueNormalDistrubtion (moremath.c:97-102): Box-Muller cos branch in double */
+__device__ __forceinline__ float random_normal(unsigned &s)
+{
+    float theta = (float)(2 * 3.14159265 * (double)random_value(s));
+    float rho = (float)__builtin_sqrt(-2 * ::log((double)random_value(s)));
+    return (float)((double)rho * ::cos((double)theta));
+}
+/* RandomDiretion (moremath.c:104-108), components drawn x, y, z */
+__device__ __forceinline__ V3 random_direction(unsigned &s)
+{
+    float a = random_normal(s);
+    float b = random_normal(s);
+    float c = random_normal(s);
+    return normalized(V3{a, b, c});
+}
+
+/* powf for the environment (raytracing.c:153,155): evaluated in double and rounded once.  glibc's powf
+ * is within 0.82 ulp, so the two differ by at most 1 ulp on a small fraction of arguments (covered by
+ * the float tolerance; measured in tests/test_gpu_parity.py). */
+__device__ __forceinline__ float pow_ref(float x, float y)
+{
+    if (y == 0.f || x == 1.f)
+        return 1.f;
+    return (float)::exp2((double)y * ::log2((double)x));
+}
+
+struct EnvParams {
+    V3 sun, horizon, zenith, ground;
+    float focus, intensity;
+};
+
+/* getEnvironmentLight (raytracing.c:151-160) */
+__device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
+{
+    float skyGradientT = pow_ref(smoothstep(0.f, 0.74f, -dir.y), 0.35f);
+    V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
+    float sun = pow_ref(fmaxf(0.f, dot(dir, s.sun)), s.focus) * s.intensity;
+    float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
+    float sunMask = dir.y < 0.f ? 1.f : 0.f;
+    float sv = sun * sunMask;
+    return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
+}
+
+/* EPSILON is the double 0.001 (scene.h:37); for any float v, v < 0.001 <=> v < 0.001f and
+ * -0.001 < v <=> -0.001f < v, so the float compares below are exact restatements. */
+constexpr float kEps = 0.001f;
+
+/* rayTriangle (raytracing.c:186-214) with the edges AB = B-A, AC = C-A precomputed (the same f32
+ * subtraction the reference performs per call).  Returns dst if hit, else a negative sentinel. */
+__device__ __forceinline__ bool ray_triangle(V3 pos, V3 dir, V3 A, V3 AB, V3 AC, V3 N, float &dstOut)
+{
+    if (dot(dir, N) >= 0.f)
+        return false;
+    V3 h = cross(dir, AC);
+    float det = dot(AB, h);
+    if (-kEps < det && det < kEps)
+        return false;
+    float invDet = 1.f / det;
+    V3 s = sub(pos, A);
+    float u = dot(s, h) * invDet;
+    if (u < 0.f || u > 1.f)
+        return false;
+    V3 q = cross(s, AB);
+    float v = dot(dir, q) * invDet;
+    if (v < 0.f || u + v > 1.f)
+        return false;
+    float dst = dot(AC, q) * invDet;
+    if (dst < kEps)
+        return false;
+    dstOut = dst;
+    return true;
+}
+
+/* raySphere (raytracing.c:162-184) -- distance only; the normal is formed by the caller when this
+ * sphere wins (it is a function of the same hitPoint = pos + dir*dst). */
+__device__ __forceinline__ bool ray_sphere(V3 pos, V3 dir, V3 c, float radius, float &dstOut)
+{
+    V3 offset = sub(pos, c);
+    float b = dot(offset, dir);
+    float cc = dot(offset, offset) - radius * radius;
+    float delta = b * b - cc;
+    if (delta < 0.f)
+        return false;
+    delta = (float)__builtin_sqrt((double)delta);
+    float dst = -b - delta;
+    if (dst < kEps)
+        dst = -b + delta;
+    if (dst < kEps)
+        return false;
+    dstOut = dst;
+    return true;
+}
+
+/* floatToUint (moremath.c:25-30); NaN -> 0 like the x86-64 build of the reference */
+__device__ __forceinline__ unsigned char float_to_u8(float f)
+{
+    if (f < 0.f)
+        return 0;
+    if (f >= 1.f)
+        return 255;
+    if (f != f)
+        return 0;
+    return (unsigned char)(unsigned)(f * 255.f);
+}
+
+} // namespace rtcdev

@@ -1,0 +1,871 @@
+/*
+ * rtc_render.hip -- the MI355X render path behind include/rtc.h.
+ *
+ * Replaces the reference's render region main.c:263-304: rowThread (main.c:81-104) fanned out over 12
+ * pthreads, each pixel running accumulationCount x calcColor (raytracing.c:262-296) over a brute-force
+ * calculateRayCollision (raytracing.c:216-240).
+ *
+ * Design:
+ *  - one lane per pixel, a 256-thread workgroup = 16x16 pixels, each wave an 8x8 tile (coherent primary
+ *    rays for the wave-uniform early-outs);
+ *  - each lane runs its pixel's samples sequentially (the RNG state x + y*W advances across samples,
+ *    main.c:95, so samples of one pixel cannot be split) as a segment state machine: every iteration of
+ *    the wave loop is ONE closest-hit query for every live lane, so the triangle loop is always
+ *    wave-uniform and triangles are read with scalar loads (SGPR operands, no LDS/VGPR traffic);
+ *  - triangles are stored with the edges AB, AC precomputed (bit-exact: the same f32 subtraction);
+ *  - quantisation (vec3ToColor) is fused; the float accumulator is written only when asked for.
+ */
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/rtc.h"
+#include "rtc_device.h"
+#include "rtc_internal.h"
+
+static_assert(sizeof(vec3) == 12, "vec3 layout");
+static_assert(sizeof(Material) == 20, "Material layout");
+static_assert(sizeof(Sphere) == 36, "Sphere layout");
+static_assert(sizeof(Triangle) == 68, "Triangle layout");
+static_assert(sizeof(Scene) == 56, "Scene layout");
+static_assert(sizeof(Color) == 3, "Color layout");
+static_assert(sizeof(Ray) == 24, "Ray layout");
+
+using namespace rtcdev;
+
+/* ---- errors ---------------------------------------------------------------------------------------- */
+static thread_local char g_err[1024] = "";
+
+extern "C" int rtc_fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+extern "C" void rtc_log(int level, const char *fmt, ...)
+{
+    const char *v = getenv("RTC_VERBOSE");
+    if (!v || atoi(v) < level)
+        return;
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+}
+
+extern "C" const char *rtc_last_error(void) { return g_err; }
+extern "C" const char *rtc_version(void) { return "rtc-mi355x 0.1 (gfx950)"; }
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return rtc_fail(-(int)e_, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                            __LINE__);                                                                 \
+    } while (0)
+
+extern "C" int rtc_device_count(int *count)
+{
+    if (!count)
+        return rtc_fail(RTC_EINVAL, "null count");
+    *count = 0;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return rtc_fail(RTC_ENODEV, "no HIP device: %s", hipGetErrorString(e));
+    *count = n;
+    return 0;
+}
+
+/* ---- device scene layout ------------------------------------------------------------------------- */
+/* 64 B per triangle, read wave-uniformly by s_load_dwordx16: A, AB, AC, N (the reference's stored normal). */
+struct __attribute__((aligned(64))) DevTri {
+    float ax, ay, az, abx, aby, abz, acx, acy, acz, nx, ny, nz, pad0, pad1, pad2, pad3;
+};
+/* material, read only for the winning triangle */
+struct __attribute__((aligned(32))) DevMat {
+    float r, g, b, emission, smoothness, pad0, pad1, pad2;
+};
+struct __attribute__((aligned(16))) DevSphere {
+    float cx, cy, cz, radius, r, g, b, emission, smoothness, pad0, pad1, pad2;
+};
+
+struct RtcDeviceScene {
+    int device;
+    int triCount, sphereCount;
+    DevTri *tris;
+    DevMat *mats;
+    DevSphere *spheres;
+};
+
+static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
+                       std::vector<DevMat> &dm, std::vector<DevSphere> &ds)
+{
+    dt.resize(triCount > 0 ? triCount : 1);
+    dm.resize(triCount > 0 ? triCount : 1);
+    for (int i = 0; i < triCount; ++i) {
+        const Triangle &t = tris[i];
+        DevTri &d = dt[i];
+        memset(&d, 0, sizeof d);
+        d.ax = t.posA.x;
+        d.ay = t.posA.y;
+        d.az = t.posA.z;
+        /* raytracing.c:191-192 minus(posB, posA), minus(posC, posA): same f32 ops */
+        d.abx = t.posB.x - t.posA.x;
+        d.aby = t.posB.y - t.posA.y;
+        d.abz = t.posB.z - t.posA.z;
+        d.acx = t.posC.x - t.posA.x;
+        d.acy = t.posC.y - t.posA.y;
+        d.acz = t.posC.z - t.posA.z;
+        d.nx = t.normal.x;
+        d.ny = t.normal.y;
+        d.nz = t.normal.z;
+        DevMat &m = dm[i];
+        memset(&m, 0, sizeof m);
+        m.r = t.mat.color.x;
+        m.g = t.mat.color.y;
+        m.b = t.mat.color.z;
+        m.emission = t.mat.emissionStrength;
+        m.smoothness = t.mat.smoothness;
+    }
+    ds.resize(sphCount > 0 ? sphCount : 1);
+    for (int i = 0; i < sphCount; ++i) {
+        DevSphere &d = ds[i];
+        memset(&d, 0, sizeof d);
+        d.cx = sph[i].pos.x;
+        d.cy = sph[i].pos.y;
+        d.cz = sph[i].pos.z;
+        d.radius = sph[i].r;
+        d.r = sph[i].mat.color.x;
+        d.g = sph[i].mat.color.y;
+        d.b = sph[i].mat.color.z;
+        d.emission = sph[i].mat.emissionStrength;
+        d.smoothness = sph[i].mat.smoothness;
+    }
+}
+
+extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount, int device,
+                                RtcDeviceScene **out)
+{
+    if (!out || triCount < 0 || sphereCount < 0 || (triCount > 0 && !tris) || (sphereCount > 0 && !spheres))
+        return rtc_fail(RTC_EINVAL, "rtc_scene_upload: bad argument");
+    *out = nullptr;
+    int n = 0;
+    int rc = rtc_device_count(&n);
+    if (rc)
+        return rc;
+    if (device < 0)
+        HIP_TRY(hipGetDevice(&device));
+    if (device >= n)
+        return rtc_fail(RTC_EINVAL, "device %d out of range (%d devices)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    std::vector<DevTri> dt;
+    std::vector<DevMat> dm;
+    std::vector<DevSphere> ds;
+    pack_scene(tris, triCount, spheres, sphereCount, dt, dm, ds);
+    RtcDeviceScene *s = new RtcDeviceScene();
+    s->device = device;
+    s->triCount = triCount;
+    s->sphereCount = sphereCount;
+    hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->spheres, ds.size() * sizeof(DevSphere));
+    if (e == hipSuccess)
+        e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(s->mats, dm.data(), dm.size() * sizeof(DevMat), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(s->spheres, ds.data(), ds.size() * sizeof(DevSphere), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        rtc_scene_release(s);
+        return rtc_fail(-(int)e, "scene upload failed: %s", hipGetErrorString(e));
+    }
+    *out = s;
+    return 0;
+}
+
+extern "C" int rtc_scene_release(RtcDeviceScene *s)
+{
+    if (!s)
+        return 0;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(s->device);
+    if (s->tris)
+        (void)hipFree(s->tris);
+    if (s->mats)
+        (void)hipFree(s->mats);
+    if (s->spheres)
+        (void)hipFree(s->spheres);
+    if (cur >= 0)
+        (void)hipSetDevice(cur);
+    delete s;
+    return 0;
+}
+
+extern "C" int rtc_rows_selected(const RtcRenderDesc *d)
+{
+    if (!d || d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height || d->height <= 0)
+        return 0;
+    return (d->height - d->rowStart + d->rowStride - 1) / d->rowStride;
+}
+
+/* ---- the render kernel ---------------------------------------------------------------------------- */
+struct RenderParams {
+    const DevTri *__restrict__ tris;
+    const DevMat *__restrict__ mats;
+    const DevSphere *__restrict__ spheres;
+    unsigned char *__restrict__ colors;
+    float *__restrict__ accum;
+    unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced */
+    int triCount, sphereCount;
+    int width, height, rows, rowStart, rowStride;
+    int spp, maxBounce;
+    int hoist;
+    float invSpp; /* (float)(1. / accumulationCount), main.c:99 */
+    V3 origin, ex, ey, ez;
+    float fov;
+    EnvParams env;
+};
+
+constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
+
+struct Closest {
+    float dst;
+    int idx; /* -1 none; 0..S-1 sphere; S.. triangle (S + t) */
+};
+
+/* calculateRayCollision (raytracing.c:216-240): spheres first (only if !trianglesOnly), then triangles
+ * in index order; a candidate replaces the current one only if strictly closer (ties keep the lower
+ * index).  The loop trip counts are kernel arguments, so the triangle index is wave-uniform and its
+ * record is fetched with scalar loads. */
+template <bool SPHERES>
+__device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir)
+{
+    Closest c{999999.f, -1};
+    if (SPHERES) {
+        for (int i = 0; i < P.sphereCount; ++i) {
+            const DevSphere sp = P.spheres[i];
+            float d;
+            if (ray_sphere(pos, dir, V3{sp.cx, sp.cy, sp.cz}, sp.radius, d) && d < c.dst) {
+                c.dst = d;
+                c.idx = i;
+            }
+        }
+    }
+    const int base = SPHERES ? P.sphereCount : 0;
+    for (int t = 0; t < P.triCount; ++t) {
+        const DevTri T = P.tris[t];
+        float d;
+        if (ray_triangle(pos, dir, V3{T.ax, T.ay, T.az}, V3{T.abx, T.aby, T.abz}, V3{T.acx, T.acy, T.acz},
+                         V3{T.nx, T.ny, T.nz}, d) &&
+            d < c.dst) {
+            c.dst = d;
+            c.idx = base + t;
+        }
+    }
+    return c;
+}
+
+template <bool SPHERES>
+__global__ __launch_bounds__(kBlock) void rtc_render_kernel(RenderParams P)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * kTileH + (wave >> 1) * 8 + (lane >> 3);
+    const bool valid = x < P.width && r < P.rows;
+    const int y = P.rowStart + r * P.rowStride;
+
+    /* rowThread primary ray (main.c:88-94): integer halves, then int->float, f32 divide */
+    const float dx = (float)(x - P.width / 2) / (float)(P.height / 2);
+    const float dy = (float)(y - P.height / 2) / (float)(P.height / 2);
+    const V3 pdir = normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
+    unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
+
+    V3 acc{0.f, 0.f, 0.f};
+    bool alive = valid && P.spp > 0 && P.maxBounce > 0;
+    int sample = 0, bounce = 0;
+    V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+    unsigned segCalls = 0, segTraced = 0;
+
+    /* bit-exact primary-hit hoisting: the primary ray consumes no RNG, so its closest hit
+     * is a function of the pixel; trace it once instead of once per sample. */
+    Closest primary{999999.f, -1};
+    if (P.hoist && alive) {
+        primary = closest_hit<SPHERES>(P, pos, dir);
+        segTraced++;
+    }
+
+    while (__any(alive)) {
+        if (alive) {
+            Closest c;
+            segCalls++;
+            if (P.hoist && bounce == 0) {
+                c = primary;
+            } else {
+                c = closest_hit<SPHERES>(P, pos, dir);
+                segTraced++;
+            }
+            bool endSample;
+            if (c.idx >= 0) {
+                /* closest.hitPoint = ray.pos + ray.dir * closest.dst (raytracing.c:238) */
+                const V3 hitPoint = add(pos, mul(dir, c.dst));
+                V3 normal, color;
+                float emission, smoothness;
+                if (SPHERES && c.idx < P.sphereCount) {
+                    const DevSphere sp = P.spheres[c.idx];
+                    normal = normalized(sub(hitPoint, V3{sp.cx, sp.cy, sp.cz})); /* raytracing.c:182 */
+                    color = V3{sp.r, sp.g, sp.b};
+                    emission = sp.emission;
+                    smoothness = sp.smoothness;
+                } else {
+                    const int t = c.idx - (SPHERES ? P.sphereCount : 0);
+                    const DevTri T = P.tris[t];
+                    const DevMat M = P.mats[t];
+                    normal = V3{T.nx, T.ny, T.nz};
+                    color = V3{M.r, M.g, M.b};
+                    emission = M.emission;
+                    smoothness = M.smoothness;
+                }
+                /* calcColor hit branch, raytracing.c:274-287 */
+                const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+                const V3 specularDir = reflect(dir, normal);
+                dir = lerp(diffuseDir, specularDir, smoothness);
+                pos = hitPoint;
+                const V3 emitted = mul(color, emission);
+                light = add(light, mulv(emitted, rayColor));
+                rayColor = mulv(rayColor, color);
+                const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                endSample = p < random_value(rng);
+                if (!endSample) {
+                    rayColor = mul(rayColor, 1.f / p);
+                    bounce++;
+                    endSample = bounce >= P.maxBounce;
+                }
+            } else {
+                /* miss branch, raytracing.c:291 */
+                light = add(light, mulv(environment(dir, P.env), rayColor));
+                endSample = true;
+            }
+            if (endSample) {
+                /* main.c:99: acc = acc + calcColor(...) * (float)(1./spp) */
+                acc = add(acc, mul(light, P.invSpp));
+                sample++;
+                if (sample >= P.spp) {
+                    alive = false;
+                } else {
+                    pos = P.origin;
+                    dir = pdir;
+                    rayColor = V3{1.f, 1.f, 1.f};
+                    light = V3{0.f, 0.f, 0.f};
+                    bounce = 0;
+                }
+            }
+        }
+    }
+
+    if (valid) {
+        const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
+        /* vec3ToColor (raytracing.c:11-15) fused */
+        P.colors[3 * o] = float_to_u8(acc.x);
+        P.colors[3 * o + 1] = float_to_u8(acc.y);
+        P.colors[3 * o + 2] = float_to_u8(acc.z);
+        if (P.accum) {
+            P.accum[3 * o] = acc.x;
+            P.accum[3 * o + 1] = acc.y;
+            P.accum[3 * o + 2] = acc.z;
+        }
+    }
+    if (P.segments) {
+        unsigned long long a = segCalls, b = segTraced;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.segments[0], a);
+            atomicAdd(&P.segments[1], b);
+        }
+    }
+}
+
+static EnvParams env_of(const Scene &s)
+{
+    EnvParams e;
+    e.sun = V3{s.normalizedSunDirection.x, s.normalizedSunDirection.y, s.normalizedSunDirection.z};
+    e.horizon = V3{s.skyColorHorizon.x, s.skyColorHorizon.y, s.skyColorHorizon.z};
+    e.zenith = V3{s.skyColorZenith.x, s.skyColorZenith.y, s.skyColorZenith.z};
+    e.ground = V3{s.groundColor.x, s.groundColor.y, s.groundColor.z};
+    e.focus = s.sunFocus;
+    e.intensity = s.sunIntensity;
+    return e;
+}
+
+__host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
+
+extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
+                                     const RtcRenderDesc *d, void *dColors, float *dAccum,
+                                     unsigned long long *dSegments, void *stream)
+{
+    if (!s || !scene || !cam || !d || !dColors)
+        return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: null argument");
+    if (d->width <= 0 || d->height <= 0 || d->rowStride <= 0 || d->rowStart < 0)
+        return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: bad geometry %dx%d rows %d+k*%d", d->width, d->height,
+                        d->rowStart, d->rowStride);
+    if ((long long)d->width * d->height > (1ll << 31) / 4)
+        return rtc_fail(RTC_EINVAL, "frame too large");
+    const int rows = rtc_rows_selected(d);
+    if (rows == 0)
+        return 0;
+    RenderParams P;
+    memset(&P, 0, sizeof P);
+    P.tris = s->tris;
+    P.mats = s->mats;
+    P.spheres = s->spheres;
+    P.colors = (unsigned char *)dColors;
+    P.accum = dAccum;
+    P.segments = dSegments;
+    P.triCount = s->triCount;
+    P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
+    P.width = d->width;
+    P.height = d->height;
+    P.rows = rows;
+    P.rowStart = d->rowStart;
+    P.rowStride = d->rowStride;
+    P.spp = d->spp;
+    P.maxBounce = d->maxBounce;
+    P.hoist = (d->flags & RTC_F_HOIST_PRIMARY) ? 1 : 0;
+    P.invSpp = d->spp > 0 ? (float)(1. / (double)d->spp) : 0.f;
+    P.origin = v3(cam->origin);
+    P.ex = v3(cam->ex);
+    P.ey = v3(cam->ey);
+    P.ez = v3(cam->ez);
+    P.fov = cam->fov;
+    P.env = env_of(*scene);
+    dim3 grid((d->width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
+    hipStream_t st = (hipStream_t)stream;
+    if (P.sphereCount > 0)
+        hipLaunchKernelGGL(rtc_render_kernel<true>, grid, dim3(kBlock), 0, st, P);
+    else
+        hipLaunchKernelGGL(rtc_render_kernel<false>, grid, dim3(kBlock), 0, st, P);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+/* ---- row de-interleave after a gather (bytes) ----------------------------------------------------- */
+__global__ __launch_bounds__(256) void rtc_deinterleave_kernel(const unsigned char *__restrict__ in, int parts,
+                                                                int rowsPerPart, int rowBytes, int height,
+                                                                unsigned char *__restrict__ out)
+{
+    /* one block-row per output row; 16-B vectors when the row is 16-B aligned */
+    const int y = blockIdx.y;
+    if (y >= height)
+        return;
+    const int g = y % parts, k = y / parts;
+    const unsigned char *src = in + ((size_t)g * rowsPerPart + k) * (size_t)rowBytes;
+    unsigned char *dst = out + (size_t)y * rowBytes;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rowBytes; i += gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+extern "C" int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,
+                                      void *dOut, void *stream)
+{
+    if (!dCompact || !dOut || parts <= 0 || width <= 0 || height <= 0 || rowsPerPart * parts < height)
+        return rtc_fail(RTC_EINVAL, "rtc_deinterleave_async: bad argument");
+    const int rowBytes = width * 3;
+    dim3 grid((rowBytes + 255) / 256 < 8 ? (rowBytes + 255) / 256 : 8, height);
+    hipLaunchKernelGGL(rtc_deinterleave_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char *)dCompact, parts, rowsPerPart, rowBytes, height, (unsigned char *)dOut);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+/* ---- host-buffer render (the main.c:263-304 seam) ------------------------------------------------- */
+template <typename T> struct DevBuf {
+    T *p = nullptr;
+    ~DevBuf()
+    {
+        if (p)
+            (void)hipFree(p);
+    }
+};
+
+extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                          const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int device,
+                          Color *outImage, float *outAccum, RtcStats *stats)
+{
+    auto t0 = std::chrono::steady_clock::now();
+    if (!scene || !cam || !d || !outImage)
+        return rtc_fail(RTC_EINVAL, "rtc_render: null argument");
+    RtcDeviceScene *s = nullptr;
+    int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, device, &s);
+    if (rc)
+        return rc;
+    struct Guard {
+        RtcDeviceScene *s;
+        ~Guard() { rtc_scene_release(s); }
+    } guard{s};
+    const int rows = rtc_rows_selected(d);
+    const size_t px = (size_t)rows * (size_t)(d->width > 0 ? d->width : 0);
+    DevBuf<unsigned char> dColors;
+    DevBuf<float> dAccum;
+    DevBuf<unsigned long long> dSeg;
+    HIP_TRY(hipMalloc(&dColors.p, px * 3 + 16));
+    if (outAccum)
+        HIP_TRY(hipMalloc(&dAccum.p, px * 3 * sizeof(float) + 16));
+    HIP_TRY(hipMalloc(&dSeg.p, 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dSeg.p, 0, 2 * sizeof(unsigned long long)));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, nullptr));
+    rc = rtc_render_rows_async(s, scene, cam, d, dColors.p, dAccum.p, dSeg.p, nullptr);
+    if (rc) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(e1, nullptr));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_TRY(hipMemcpy(outImage, dColors.p, px * 3, hipMemcpyDeviceToHost));
+    if (outAccum)
+        HIP_TRY(hipMemcpy(outAccum, dAccum.p, px * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    unsigned long long seg[2] = {0, 0};
+    HIP_TRY(hipMemcpy(seg, dSeg.p, sizeof seg, hipMemcpyDeviceToHost));
+    if (stats) {
+        stats->renderMs = ms;
+        stats->segments = seg[0];
+        stats->samples = (unsigned long long)px * (unsigned long long)(d->spp > 0 ? d->spp : 0);
+        stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return 0;
+}
+
+extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                                const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
+                                Color *outImage, float *outAccum, RtcStats *stats)
+{
+    auto t0 = std::chrono::steady_clock::now();
+    if (!scene || !cam || !d || !outImage || numDevices <= 0 || d->rowStart != 0 || d->rowStride != 1)
+        return rtc_fail(RTC_EINVAL, "rtc_render_multi: bad argument (full frames only)");
+    int n = 0;
+    if (int rc = rtc_device_count(&n))
+        return rc;
+    if (numDevices > n)
+        return rtc_fail(RTC_EINVAL, "rtc_render_multi: %d devices requested, %d present", numDevices, n);
+    struct Part {
+        RtcDeviceScene *s = nullptr;
+        unsigned char *col = nullptr;
+        float *acc = nullptr;
+        unsigned long long *seg = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        int rows = 0;
+    };
+    std::vector<Part> parts(numDevices);
+    auto cleanup = [&]() {
+        for (int g = 0; g < numDevices; ++g) {
+            Part &p = parts[g];
+            (void)hipSetDevice(g);
+            if (p.col)
+                (void)hipFree(p.col);
+            if (p.acc)
+                (void)hipFree(p.acc);
+            if (p.seg)
+                (void)hipFree(p.seg);
+            if (p.e0)
+                (void)hipEventDestroy(p.e0);
+            if (p.e1)
+                (void)hipEventDestroy(p.e1);
+            if (p.st)
+                (void)hipStreamDestroy(p.st);
+            rtc_scene_release(p.s);
+        }
+    };
+    int rc = 0;
+    for (int g = 0; g < numDevices && !rc; ++g) {
+        Part &p = parts[g];
+        RtcRenderDesc dg = *d;
+        dg.rowStart = g;
+        dg.rowStride = numDevices;
+        p.rows = rtc_rows_selected(&dg);
+        rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s);
+        if (rc)
+            break;
+        const size_t px = (size_t)p.rows * (size_t)d->width;
+        hipError_t e = hipStreamCreate(&p.st);
+        if (e == hipSuccess)
+            e = hipMalloc(&p.col, px * 3 + 16);
+        if (e == hipSuccess && outAccum)
+            e = hipMalloc(&p.acc, px * 3 * sizeof(float) + 16);
+        if (e == hipSuccess)
+            e = hipMalloc(&p.seg, 2 * sizeof(unsigned long long));
+        if (e == hipSuccess)
+            e = hipMemsetAsync(p.seg, 0, 2 * sizeof(unsigned long long), p.st);
+        if (e == hipSuccess)
+            e = hipEventCreate(&p.e0);
+        if (e == hipSuccess)
+            e = hipEventCreate(&p.e1);
+        if (e == hipSuccess)
+            e = hipEventRecord(p.e0, p.st);
+        if (e != hipSuccess) {
+            rc = rtc_fail(-(int)e, "rtc_render_multi setup on device %d: %s", g, hipGetErrorString(e));
+            break;
+        }
+        rc = rtc_render_rows_async(p.s, scene, cam, &dg, p.col, p.acc, p.seg, p.st);
+        if (!rc && (e = hipEventRecord(p.e1, p.st)) != hipSuccess)
+            rc = rtc_fail(-(int)e, "event record: %s", hipGetErrorString(e));
+    }
+    double maxMs = 0;
+    unsigned long long segs = 0;
+    std::vector<unsigned char> col;
+    std::vector<float> acc;
+    for (int g = 0; g < numDevices && !rc; ++g) {
+        Part &p = parts[g];
+        (void)hipSetDevice(g);
+        hipError_t e = hipEventSynchronize(p.e1);
+        float ms = 0;
+        if (e == hipSuccess)
+            e = hipEventElapsedTime(&ms, p.e0, p.e1);
+        const size_t px = (size_t)p.rows * (size_t)d->width;
+        col.resize(px * 3 + 1);
+        unsigned long long sg[2] = {0, 0};
+        if (e == hipSuccess)
+            e = hipMemcpy(col.data(), p.col, px * 3, hipMemcpyDeviceToHost);
+        if (e == hipSuccess)
+            e = hipMemcpy(sg, p.seg, sizeof sg, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && outAccum) {
+            acc.resize(px * 3 + 1);
+            e = hipMemcpy(acc.data(), p.acc, px * 3 * sizeof(float), hipMemcpyDeviceToHost);
+        }
+        if (e != hipSuccess) {
+            rc = rtc_fail(-(int)e, "rtc_render_multi readback from device %d: %s", g, hipGetErrorString(e));
+            break;
+        }
+        if (ms > maxMs)
+            maxMs = ms;
+        segs += sg[0];
+        const size_t rowB = (size_t)d->width * 3;
+        for (int k = 0; k < p.rows; ++k) {
+            const int y = g + k * numDevices;
+            memcpy((unsigned char *)outImage + (size_t)y * rowB, col.data() + (size_t)k * rowB, rowB);
+            if (outAccum)
+                memcpy(outAccum + (size_t)y * rowB, acc.data() + (size_t)k * rowB, rowB * sizeof(float));
+        }
+    }
+    cleanup();
+    if (rc)
+        return rc;
+    if (stats) {
+        stats->renderMs = maxMs;
+        stats->segments = segs;
+        stats->samples = (unsigned long long)d->width * d->height * (unsigned long long)(d->spp > 0 ? d->spp : 0);
+        stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return 0;
+}
+
+/* ---- probes: single reference functions on the device, for known-answer tests ---------------------- */
+__global__ void probe_tri_kernel(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const Ray R = rays[i];
+    const Triangle T = tris[i];
+    const V3 A = v3(T.posA);
+    float d = 0.f;
+    bool h = ray_triangle(v3(R.pos), v3(R.dir), A, sub(v3(T.posB), A), sub(v3(T.posC), A), v3(T.normal), d);
+    didHit[i] = h ? 1 : 0;
+    dst[i] = h ? d : 0.f;
+}
+
+__global__ void probe_sphere_kernel(const Ray *rays, const Sphere *sph, size_t n, int *didHit, float *dst,
+                                    vec3 *normal)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const Ray R = rays[i];
+    const Sphere S = sph[i];
+    float d = 0.f;
+    bool h = ray_sphere(v3(R.pos), v3(R.dir), v3(S.pos), S.r, d);
+    didHit[i] = h ? 1 : 0;
+    dst[i] = h ? d : 0.f;
+    V3 nrm{0.f, 0.f, 0.f};
+    if (h)
+        nrm = normalized(sub(add(v3(R.pos), mul(v3(R.dir), d)), v3(S.pos)));
+    normal[i] = vec3{nrm.x, nrm.y, nrm.z};
+}
+
+__global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n, vec3 *out)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    Scene s = scenes[i];
+    EnvParams e;
+    e.sun = v3(s.normalizedSunDirection);
+    e.horizon = v3(s.skyColorHorizon);
+    e.zenith = v3(s.skyColorZenith);
+    e.ground = v3(s.groundColor);
+    e.focus = s.sunFocus;
+    e.intensity = s.sunIntensity;
+    V3 c = environment(v3(rays[i].dir), e);
+    out[i] = vec3{c.x, c.y, c.z};
+}
+
+__global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, float *uni, float *nrm, vec3 *dirs)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    unsigned s = seeds[i];
+    for (int k = 0; k < draws; ++k)
+        uni[i * draws + k] = random_value(s);
+    s = seeds[i];
+    for (int k = 0; k < draws; ++k)
+        nrm[i * draws + k] = random_normal(s);
+    s = seeds[i];
+    for (int k = 0; k < draws; ++k) {
+        V3 d = random_direction(s);
+        dirs[i * draws + k] = vec3{d.x, d.y, d.z};
+    }
+}
+
+namespace {
+struct Scratch {
+    std::vector<void *> ptrs;
+    ~Scratch()
+    {
+        for (void *p : ptrs)
+            (void)hipFree(p);
+    }
+    hipError_t alloc(void **p, size_t bytes)
+    {
+        hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+        if (e == hipSuccess)
+            ptrs.push_back(*p);
+        return e;
+    }
+};
+int probe_prelude()
+{
+    int n = 0;
+    return rtc_device_count(&n);
+}
+} // namespace
+
+#define ALLOC_IN(dptr, hptr, bytes)                                                                    \
+    HIP_TRY(sc.alloc((void **)&dptr, bytes));                                                          \
+    HIP_TRY(hipMemcpy(dptr, hptr, bytes, hipMemcpyHostToDevice))
+#define ALLOC_OUT(dptr, bytes) HIP_TRY(sc.alloc((void **)&dptr, bytes))
+
+static unsigned probe_blocks(size_t n) { return (unsigned)((n + 255) / 256 > 0 ? (n + 255) / 256 : 1); }
+
+extern "C" int rtc_probe_ray_triangle(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst)
+{
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0)
+        return 0;
+    Scratch sc;
+    Ray *dr;
+    Triangle *dt;
+    int *dh;
+    float *dd;
+    ALLOC_IN(dr, rays, n * sizeof(Ray));
+    ALLOC_IN(dt, tris, n * sizeof(Triangle));
+    ALLOC_OUT(dh, n * sizeof(int));
+    ALLOC_OUT(dd, n * sizeof(float));
+    hipLaunchKernelGGL(probe_tri_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, dt, n, dh, dd);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(didHit, dh, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(dst, dd, n * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int rtc_probe_ray_sphere(const Ray *rays, const Sphere *spheres, size_t n, int *didHit, float *dst,
+                                    vec3 *normal)
+{
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0)
+        return 0;
+    Scratch sc;
+    Ray *dr;
+    Sphere *ds;
+    int *dh;
+    float *dd;
+    vec3 *dn;
+    ALLOC_IN(dr, rays, n * sizeof(Ray));
+    ALLOC_IN(ds, spheres, n * sizeof(Sphere));
+    ALLOC_OUT(dh, n * sizeof(int));
+    ALLOC_OUT(dd, n * sizeof(float));
+    ALLOC_OUT(dn, n * sizeof(vec3));
+    hipLaunchKernelGGL(probe_sphere_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dh, dd, dn);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(didHit, dh, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(dst, dd, n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(normal, dn, n * sizeof(vec3), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *out)
+{
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0)
+        return 0;
+    Scratch sc;
+    Ray *dr;
+    Scene *ds;
+    vec3 *dout;
+    ALLOC_IN(dr, rays, n * sizeof(Ray));
+    ALLOC_IN(ds, scenes, n * sizeof(Scene));
+    ALLOC_OUT(dout, n * sizeof(vec3));
+    hipLaunchKernelGGL(probe_env_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, n * sizeof(vec3), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
+                                vec3 *direction)
+{
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0 || draws <= 0)
+        return 0;
+    Scratch sc;
+    unsigned *dsd;
+    float *du, *dn;
+    vec3 *dd;
+    const size_t m = n * (size_t)draws;
+    ALLOC_IN(dsd, seeds, n * sizeof(unsigned));
+    ALLOC_OUT(du, m * sizeof(float));
+    ALLOC_OUT(dn, m * sizeof(float));
+    ALLOC_OUT(dd, m * sizeof(vec3));
+    hipLaunchKernelGGL(probe_random_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dsd, n, draws, du, dn, dd);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(uniform, du, m * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(normal, dn, m * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(direction, dd, m * sizeof(vec3), hipMemcpyDeviceToHost));
+    return 0;
+}

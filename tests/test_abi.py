@@ -1,0 +1,69 @@
+"""The C ABI library: loads, exports every symbol include/rtc.h declares, keeps the reference layouts, and
+fails loudly (no CPU fallback) where no GPU is visible."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO, load_tris
+
+import raytracingc_amd as rt
+from raytracingc_amd import _abi
+
+
+def declared_symbols():
+    txt = open(os.path.join(REPO, "include", "rtc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtc_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = rt.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), f"librtc.so does not export {s}"
+    assert sorted(_abi.EXPORTS) == syms
+
+
+def test_library_has_gfx950_code_object():
+    blob = open(rt.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_struct_layouts():
+    assert C.sizeof(_abi.Triangle) == 68 and C.sizeof(_abi.Sphere) == 36 and C.sizeof(_abi.Scene) == 56
+    assert C.sizeof(_abi.Ray) == 24 and C.sizeof(_abi.Material) == 20 and C.sizeof(_abi.Vec3) == 12
+    assert C.sizeof(_abi.RtcCamera) == 52 and C.sizeof(_abi.RtcRenderDesc) == 32
+
+
+def test_version_and_rows_selected():
+    assert b"gfx950" in rt.lib().rtc_version()
+    for h, start, stride, want in [(1080, 0, 1, 1080), (1080, 3, 8, 135), (1080, 7, 8, 135), (1079, 7, 8, 134), (5, 4, 8, 1),
+                                   (5, 5, 8, 0), (0, 0, 1, 0), (10, 0, 0, 0)]:
+        assert rt.RenderConfig(width=4, height=h, row_start=start, row_stride=stride).rows() == want
+
+
+def test_no_gpu_fails_loudly():
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    tris, tonly = load_tris("simplest")
+    with pytest.raises(rt.RtcError) as ei:
+        rt.render(tris, None, rt.default_scene(), rt.camera_basis(), rt.RenderConfig(8, 8, 1))
+    assert ei.value.code == _abi.RTC_ENODEV
+    with pytest.raises(rt.RtcError):
+        rt.rayTriangle(np.zeros(1, rt.RAY_DT), tris[:1])
+
+
+def test_bad_arguments_rejected():
+    L = rt.lib()
+    d = _abi.RtcRenderDesc(16, 16, 1, 10, 1, 0, 1, 0)
+    # null scene pointer etc. are argument errors, whatever the device state
+    assert L.rtc_render(None, 0, None, 0, None, None, C.byref(d), 0, None, None, None) == _abi.RTC_EINVAL
+    assert L.rtc_deinterleave_async(None, 0, 0, 0, 0, None, None) == _abi.RTC_EINVAL
+    assert L.rtc_write_bmp(b"/nonexistent/dir/x.bmp", 1, 1, None) == _abi.RTC_EINVAL
+    assert b"rtc_" in L.rtc_last_error() or len(L.rtc_last_error()) > 0
