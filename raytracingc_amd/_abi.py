@@ -125,6 +125,14 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"librtc.so not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
+    # PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7, but its libc10_hip links it by file
+    # name).  If librtc.so loaded /opt/rocm's copy first, torch would load a second HIP runtime and see no
+    # GPU.  Importing torch first makes librtc.so bind to the runtime torch already holds, so device
+    # pointers and streams are shared.  Without torch, librtc.so uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, ip, sz = C.c_void_p, C.c_int, C.c_size_t
     L.rtc_last_error.restype = C.c_char_p
