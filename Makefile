@@ -11,7 +11,7 @@ LIBDIR   := raytracingc_amd/_lib
 CSRC     := raytracingc_amd/csrc
 REF      ?= /root/reference
 
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fno-slp-vectorize -fPIC -std=c++17 -Wall
 CFLAGS   := -std=gnu11 -O2 -fPIC -ffp-contract=off -Wall -Wextra
 
 LIB      := $(LIBDIR)/librtc.so
@@ -33,6 +33,16 @@ $(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_i
 $(LIB): $(BUILD)/rtc_render.o $(BUILD)/scene_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so
 
+# diagnostic variant (per-wave cycle stamps); never the measured product
+DIAGLIB  := $(LIBDIR)/librtc_diag.so
+$(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -c $< -o $@
+
+$(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/scene_build.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+
+diag: $(DIAGLIB)
+
 $(BUILD)/rtc_main.o: $(CSRC)/rtc_main.c include/rtc.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
@@ -52,4 +62,4 @@ ref: | $(BUILD)
 clean:
 	rm -rf $(BUILD) $(LIB) $(CLI) $(ORACLE) $(REFBIN)
 
-.PHONY: all ref clean
+.PHONY: all ref clean diag

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "librtc.so")
+# RTC_LIB_PATH selects the diagnostic build (librtc_diag.so) for tools/kernel_probe.py only
+LIB_PATH = os.environ.get("RTC_LIB_PATH") or os.path.join(HERE, "_lib", "librtc.so")
 CLI_PATH = os.path.join(HERE, "_lib", "rtc")
 
 

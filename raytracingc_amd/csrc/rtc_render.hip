@@ -86,6 +86,11 @@ extern "C" int rtc_device_count(int *count)
 }
 
 /* ---- device scene layout ------------------------------------------------------------------------- */
+#ifndef RTC_UNROLL
+#define RTC_UNROLL 4
+#endif
+constexpr int kUnroll = RTC_UNROLL; /* records per scalar-load batch; arrays are padded to a multiple of 8 */
+static_assert(8 % kUnroll == 0, "padding assumes kUnroll divides 8");
 /* 64 B per triangle, read wave-uniformly by s_load_dwordx16: A, AB, AC, N (the reference's stored normal). */
 struct __attribute__((aligned(64))) DevTri {
     float ax, ay, az, abx, aby, abz, acx, acy, acz, nx, ny, nz, pad0, pad1, pad2, pad3;
@@ -97,20 +102,30 @@ struct __attribute__((aligned(32))) DevMat {
 struct __attribute__((aligned(16))) DevSphere {
     float cx, cy, cz, radius, r, g, b, emission, smoothness, pad0, pad1, pad2;
 };
+/* Per-frame record for primary rays (bounce 0), whose origin is the camera for every pixel: the terms of
+ * rayTriangle that depend only on the origin and the triangle -- s0 = origin - A, q0 = cross(s0, AB),
+ * dAC0 = dot(AC, q0) (raytracing.c:198,202,206) -- are computed once per launch by rtc_prep_primary with the
+ * same f32 operations, so the primary test stays bit-exact while skipping them.  64 B, scalar-loaded. */
+struct __attribute__((aligned(64))) DevPrim {
+    float nx, ny, nz, acx, acy, acz, abx, aby, abz, s0x, s0y, s0z, q0x, q0y, q0z, dac0;
+};
 
 struct RtcDeviceScene {
     int device;
-    int triCount, sphereCount;
+    int triCount, triPadded, sphereCount; /* triPadded: multiple of kUnroll, zero (never-hit) records */
     DevTri *tris;
     DevMat *mats;
     DevSphere *spheres;
+    DevPrim *prim; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
                        std::vector<DevMat> &dm, std::vector<DevSphere> &ds)
 {
-    dt.resize(triCount > 0 ? triCount : 1);
-    dm.resize(triCount > 0 ? triCount : 1);
+    const size_t padded = ((size_t)(triCount > 0 ? triCount : 0) + 7) / 8 * 8 + 8;
+    /* zero records are never hit: N = 0 makes dot(dir, N) >= 0 (or NaN, and then det is NaN too) */
+    dt.assign(padded, DevTri{});
+    dm.assign(padded, DevMat{});
     for (int i = 0; i < triCount; ++i) {
         const Triangle &t = tris[i];
         DevTri &d = dt[i];
@@ -174,12 +189,15 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     RtcDeviceScene *s = new RtcDeviceScene();
     s->device = device;
     s->triCount = triCount;
+    s->triPadded = (triCount + kUnroll - 1) / kUnroll * kUnroll;
     s->sphereCount = sphereCount;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
     if (e == hipSuccess)
         e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
     if (e == hipSuccess)
         e = hipMalloc(&s->spheres, ds.size() * sizeof(DevSphere));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->prim, dt.size() * sizeof(DevPrim));
     if (e == hipSuccess)
         e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -207,6 +225,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->mats);
     if (s->spheres)
         (void)hipFree(s->spheres);
+    if (s->prim)
+        (void)hipFree(s->prim);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -225,10 +245,11 @@ struct RenderParams {
     const DevTri *__restrict__ tris;
     const DevMat *__restrict__ mats;
     const DevSphere *__restrict__ spheres;
+    const DevPrim *__restrict__ prim;
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced */
-    int triCount, sphereCount;
+    int triCount, triPadded, sphereCount;
     int width, height, rows, rowStart, rowStride;
     int spp, maxBounce;
     int hoist;
@@ -240,17 +261,143 @@ struct RenderParams {
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 
+/* rtc_prep_primary: per-launch primary-ray records (see DevPrim). */
+__global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict__ tris, DevPrim *__restrict__ prim,
+                                                        int triCount, V3 origin)
+{
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= triCount)
+        return;
+    const DevTri T = tris[t];
+    const V3 AB{T.abx, T.aby, T.abz}, AC{T.acx, T.acy, T.acz};
+    const V3 s0 = sub(origin, V3{T.ax, T.ay, T.az}); /* raytracing.c:198 */
+    const V3 q0 = cross(s0, AB);                      /* :202 */
+    DevPrim r;
+    r.nx = T.nx;
+    r.ny = T.ny;
+    r.nz = T.nz;
+    r.acx = AC.x;
+    r.acy = AC.y;
+    r.acz = AC.z;
+    r.abx = AB.x;
+    r.aby = AB.y;
+    r.abz = AB.z;
+    r.s0x = s0.x;
+    r.s0y = s0.y;
+    r.s0z = s0.z;
+    r.q0x = q0.x;
+    r.q0y = q0.y;
+    r.q0z = q0.z;
+    r.dac0 = dot(AC, q0); /* :206 numerator */
+    prim[t] = r;
+}
+
 struct Closest {
     float dst;
     int idx; /* -1 none; 0..S-1 sphere; S.. triangle (S + t) */
 };
 
+/* Exact-safe rejection filter.  With r = rcp(det) (<= 1 ulp) the approximations ua = uu*r, va = vv*r,
+ * da = dd*r are within 2^-21 relative of the reference's u, v, dst (raytracing.c:197-207, invDet = 1/det
+ * rounded), so each failed comparison below implies the corresponding reference rejection:
+ *   ua < -2^-60 => u < 0;  va < -2^-60 => v < 0;  ua+va > 1+1e-5 (ua, va >= -2^-60) => u+v > 1 or u > 1;
+ *   da < 0.00099 => dst < EPSILON.
+ * The 2^-60 floor keeps the sign tests away from products that could round to -0 (no rejection in the
+ * reference).  Every comparison is written so that NaN keeps the lane a candidate: the exact path then
+ * decides as the reference does. */
+constexpr float kTiny = 8.67361738e-19f; /* 2^-60 */
+
+__device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
+{
+    return !(ua < -kTiny) & !(va < -kTiny) & !(ua + va > 1.00001f) & !(da < 0.00099f);
+}
+
+
+
+/* Primary segments (every live lane at bounce 0, pos == camera origin): rayTriangle with the per-launch
+ * records.  A batch of kUnroll records is scalar-loaded at once (SGPR operands, no VGPR/LDS traffic); the
+ * common path is two wave-uniform branches per triangle -- back face, then the exact-safe filter -- so the
+ * scalar unit (exec-mask bookkeeping) does not become the limiter. */
+__device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, Closest &c, int base)
+{
+    const int Tp = P.triPadded;
+    for (int t0 = 0; t0 < Tp; t0 += kUnroll) {
+        DevPrim RR[kUnroll];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            RR[k] = P.prim[t0 + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            const DevPrim &R = RR[k];
+            /* backface cull on the stored normal (raytracing.c:189) */
+            const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
+            if (!(nd >= 0.f)) {
+                const V3 h = cross(dir, V3{R.acx, R.acy, R.acz});
+                const float det = dot(V3{R.abx, R.aby, R.abz}, h);
+                const float uu = dot(V3{R.s0x, R.s0y, R.s0z}, h);
+                const float vv = dot(dir, V3{R.q0x, R.q0y, R.q0z});
+                const float r = __builtin_amdgcn_rcpf(det);
+                const bool detOk = !(-kEps < det && det < kEps);
+                if (detOk & maybe_hit(uu * r, vv * r, R.dac0 * r)) {
+                    /* the reference's arithmetic from here on (raytracing.c:197-208) */
+                    const float invDet = 1.f / det;
+                    const float u = uu * invDet;
+                    const float v = vv * invDet;
+                    const float dst = R.dac0 * invDet;
+                    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                        c.dst = dst;
+                        c.idx = base + t0 + k;
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* General segments (any origin): rayTriangle (raytracing.c:186-214) with AB, AC precomputed. */
+__device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V3 dir, Closest &c, int base)
+{
+    const int Tp = P.triPadded;
+    for (int t0 = 0; t0 < Tp; t0 += kUnroll) {
+        DevTri RR[kUnroll];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            RR[k] = P.tris[t0 + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k) {
+            const DevTri &R = RR[k];
+            const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
+            if (!(nd >= 0.f)) {
+                const V3 AB{R.abx, R.aby, R.abz}, AC{R.acx, R.acy, R.acz};
+                const V3 h = cross(dir, AC);
+                const float det = dot(AB, h);
+                const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
+                const float uu = dot(s, h);
+                const float r = __builtin_amdgcn_rcpf(det);
+                const float ua = uu * r;
+                const bool detOk = !(-kEps < det && det < kEps);
+                if (detOk & !(ua < -kTiny) & !(ua > 1.000001f)) {
+                    const float invDet = 1.f / det;
+                    const float u = uu * invDet;
+                    const V3 q = cross(s, AB);
+                    const float v = dot(dir, q) * invDet;
+                    const float dst = dot(AC, q) * invDet;
+                    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                        c.dst = dst;
+                        c.idx = base + t0 + k;
+                    }
+                }
+            }
+        }
+    }
+}
+
 /* calculateRayCollision (raytracing.c:216-240): spheres first (only if !trianglesOnly), then triangles
  * in index order; a candidate replaces the current one only if strictly closer (ties keep the lower
  * index).  The loop trip counts are kernel arguments, so the triangle index is wave-uniform and its
- * record is fetched with scalar loads. */
+ * record is fetched with scalar loads.  `primaryWave` (wave-uniform) = every live lane is at bounce 0. */
 template <bool SPHERES>
-__device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir)
+__device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir, bool primaryWave)
 {
     Closest c{999999.f, -1};
     if (SPHERES) {
@@ -264,22 +411,34 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
         }
     }
     const int base = SPHERES ? P.sphereCount : 0;
-    for (int t = 0; t < P.triCount; ++t) {
-        const DevTri T = P.tris[t];
-        float d;
-        if (ray_triangle(pos, dir, V3{T.ax, T.ay, T.az}, V3{T.abx, T.aby, T.abz}, V3{T.acx, T.acy, T.acz},
-                         V3{T.nx, T.ny, T.nz}, d) &&
-            d < c.dst) {
-            c.dst = d;
-            c.idx = base + t;
-        }
-    }
+    if (primaryWave)
+        closest_primary(P, dir, c, base);
+    else
+        closest_general(P, pos, dir, c, base);
     return c;
 }
 
-template <bool SPHERES>
-__global__ __launch_bounds__(kBlock) void rtc_render_kernel(RenderParams P)
+#ifdef RTC_DIAG
+/* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp} */
+__device__ unsigned long long *g_rtc_diag = nullptr;
+extern "C" int rtc_diag_set_buffer(void *dptr)
 {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_diag), &dptr, sizeof dptr));
+    return 0;
+}
+#endif
+
+#ifndef RTC_MIN_WAVES
+#define RTC_MIN_WAVES 1
+#endif
+template <bool SPHERES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_WAVES))) void rtc_render_kernel(
+    RenderParams P)
+{
+#ifdef RTC_DIAG
+    const unsigned long long diagT0 = __builtin_amdgcn_s_memtime();
+    unsigned diagIters = 0;
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
@@ -303,18 +462,24 @@ __global__ __launch_bounds__(kBlock) void rtc_render_kernel(RenderParams P)
      * is a function of the pixel; trace it once instead of once per sample. */
     Closest primary{999999.f, -1};
     if (P.hoist && alive) {
-        primary = closest_hit<SPHERES>(P, pos, dir);
+        primary = closest_hit<SPHERES>(P, pos, dir, true);
         segTraced++;
     }
 
     while (__any(alive)) {
+#ifdef RTC_DIAG
+        diagIters++;
+#endif
+        /* wave-uniform: every live lane that traces this iteration is at bounce 0 (origin = camera) */
+        const bool needTrace = alive && !(P.hoist && bounce == 0);
+        const bool primaryWave = __all(!needTrace || bounce == 0);
         if (alive) {
             Closest c;
             segCalls++;
-            if (P.hoist && bounce == 0) {
+            if (!needTrace) {
                 c = primary;
             } else {
-                c = closest_hit<SPHERES>(P, pos, dir);
+                c = closest_hit<SPHERES>(P, pos, dir, primaryWave);
                 segTraced++;
             }
             bool endSample;
@@ -387,6 +552,14 @@ __global__ __launch_bounds__(kBlock) void rtc_render_kernel(RenderParams P)
             P.accum[3 * o + 2] = acc.z;
         }
     }
+#ifdef RTC_DIAG
+    if (g_rtc_diag && lane == 0) {
+        const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
+        g_rtc_diag[3 * w] = __builtin_amdgcn_s_memtime() - diagT0;
+        g_rtc_diag[3 * w + 1] = diagIters;
+        g_rtc_diag[3 * w + 2] = diagT0;
+    }
+#endif
     if (P.segments) {
         unsigned long long a = segCalls, b = segTraced;
         for (int off = 32; off > 0; off >>= 1) {
@@ -437,6 +610,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.accum = dAccum;
     P.segments = dSegments;
     P.triCount = s->triCount;
+    P.triPadded = s->triPadded;
     P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
     P.width = d->width;
     P.height = d->height;
@@ -455,6 +629,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.env = env_of(*scene);
     dim3 grid((d->width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
     hipStream_t st = (hipStream_t)stream;
+    P.prim = s->prim;
+    if (s->triPadded > 0)
+        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->prim,
+                           s->triPadded, P.origin);
     if (P.sphereCount > 0)
         hipLaunchKernelGGL(rtc_render_kernel<true>, grid, dim3(kBlock), 0, st, P);
     else

@@ -1,0 +1,89 @@
+"""Multi-rank plumbing on CPU (gloo, world_size 2 and 3): row interleave across ranks (main.c:84 lifted to
+ranks), padded compact parts, the gather to rank 0 and the re-interleave give the single-process frame.
+The per-rank renderer here is the CPU oracle (test infrastructure) standing in for the HIP kernel, which
+the -m gpu tests cover (tests/test_gpu_parity.py::test_row_partition_and_deinterleave)."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_tris, setup_from_flags
+
+from raytracingc_amd.distributed import (FrameRenderer, interleave_reference, rank_config, rows_per_rank)
+
+W, H, SPP = 40, 23, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_part(cfg_r, out):
+    import oracle.binding as orc
+    from raytracingc_amd._abi import RtcRenderDesc
+
+    tris, tonly = load_tris("fsuzane")
+    scene, cam, _ = setup_from_flags({})
+    d = RtcRenderDesc(cfg_r.width, cfg_r.height, cfg_r.spp, cfg_r.max_bounce, tonly, cfg_r.row_start,
+                      cfg_r.row_stride, 0)
+    col, _, _ = orc.render(tris, None, scene, cam, d, threads=2)
+    out.zero_()
+    out[: col.shape[0]].copy_(torch.from_numpy(col))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import raytracingc_amd as rt
+
+        cfg = rt.RenderConfig(W, H, SPP, 10, True)
+        fr = FrameRenderer(cfg, _oracle_part, torch.device("cpu"))
+        frame = fr()
+        if rank == 0:
+            q.put(frame.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_frame_equals_single_process(world):
+    import raytracingc_amd as rt
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = torch.zeros((H, W, 3), dtype=torch.uint8)
+    _oracle_part(rt.RenderConfig(W, H, SPP, 10, True), full)
+    assert np.array_equal(frame, full.numpy())
+
+
+def test_partition_helpers():
+    import raytracingc_amd as rt
+
+    for h, g in [(1080, 8), (1080, 7), (23, 3), (5, 8), (1, 1)]:
+        rows = rows_per_rank(h, g)
+        assert rows * g >= h and (rows - 1) * g < h
+        got = sorted(y for r in range(g) for y in range(r, h, g))
+        assert got == list(range(h))
+        cfg = rank_config(rt.RenderConfig(8, h), min(g - 1, h - 1), g)
+        assert cfg.rows() <= rows
+    parts = torch.arange(3 * 4 * 2 * 3, dtype=torch.int32).reshape(3, 4, 2, 3)
+    out = interleave_reference(parts, 10)
+    for y in range(10):
+        assert torch.equal(out[y], parts[y % 3, y // 3])

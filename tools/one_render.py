@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""One render of a chosen variant (for rocprofv3 counter passes).  Usage: one_render.py [variant] [reps]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import raytracingc_amd as rt  # noqa: E402
+from conftest import load_tris  # noqa: E402
+
+v = sys.argv[1] if len(sys.argv) > 1 else "faithful"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+tris, _ = load_tris("ultracomplex")
+cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
+       "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
+       "empty": rt.RenderConfig(1920, 1080, 64, 10, True)}[v]
+if v == "empty":
+    tris = tris[:0]
+for _ in range(reps):
+    _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+print(v, st["render_ms"])
