@@ -54,6 +54,7 @@ typedef struct RtcRenderDesc {
 } RtcRenderDesc;
 
 #define RTC_F_HOIST_PRIMARY 0x1  /* bit-exact: trace each pixel's primary ray once; default off */
+#define RTC_F_DEBUG_BOUNCES 0x2  /* calcDebugColor (raytracing.c:242-260) instead of calcColor: bounce-count grey */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */

@@ -38,7 +38,7 @@ def lib() -> C.CDLL:
         L.oracle_environment.restype = None
         L.oracle_random.argtypes = [vp, sz, ip, vp, vp, vp]
         L.oracle_random.restype = None
-        L.oracle_calc_color.argtypes = [vp, ip, vp, ip, C.POINTER(Scene), ip, vp, vp, vp, sz, vp, vp]
+        L.oracle_calc_color.argtypes = [vp, ip, vp, ip, C.POINTER(Scene), ip, vp, vp, vp, sz, vp, vp, ip]
         L.oracle_calc_color.restype = None
         _lib = L
     return _lib
@@ -108,7 +108,7 @@ def random_sequences(seeds, draws: int):
     return u, g, d
 
 
-def calc_color(tris, spheres, scene: Scene, triangles_only: int, rays, seeds, max_bounce):
+def calc_color(tris, spheres, scene: Scene, triangles_only: int, rays, seeds, max_bounce, debug: bool = False):
     t, nt = _arr(tris, TRIANGLE_DT)
     s, ns = _arr(spheres, SPHERE_DT)
     r = np.ascontiguousarray(rays, RAY_DT)
@@ -118,5 +118,5 @@ def calc_color(tris, spheres, scene: Scene, triangles_only: int, rays, seeds, ma
     out = np.zeros((n, 3), np.float32)
     after = np.zeros(n, np.uint32)
     lib().oracle_calc_color(_p(t), nt, _p(s), ns, C.byref(scene), triangles_only, _p(r), _p(sd), _p(mb), n, _p(out),
-                            _p(after))
+                            _p(after), int(debug))
     return out, after

@@ -234,6 +234,22 @@ int main(int argc, char **argv)
             }
             write_all(argv[a + 3], out, n * sizeof(KatCalcOut));
             return 0;
+        } else if (strcmp(argv[a], "--kat-debug") == 0 && a + 3 < argc) {
+            /* --kat-debug <mode> <in> <out>: calcDebugColor (raytracing.c:242-260), same records as --kat-calc */
+            int tonly;
+            load_scene_mode(argv[a + 1], &tonly);
+            scene.normalizedSunDirection = normalized(sunDirection);
+            size_t nb;
+            KatCalcIn *in = read_all(argv[a + 2], &nb);
+            size_t n = nb / sizeof(KatCalcIn);
+            KatCalcOut *out = calloc(n ? n : 1, sizeof(KatCalcOut));
+            for (size_t i = 0; i < n; ++i) {
+                rngState = in[i].seed;
+                out[i].color = calcDebugColor(in[i].ray, tonly, in[i].maxBounce, scene);
+                out[i].seedAfter = rngState;
+            }
+            write_all(argv[a + 3], out, n * sizeof(KatCalcOut));
+            return 0;
         } else if (strcmp(argv[a], "--dump-tris") == 0 && a + 2 < argc) {
             /* --dump-tris <mode: default|path.obj> <out> */
             int tonly;

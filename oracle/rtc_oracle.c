@@ -13,6 +13,7 @@
  *   rayTriangle          raytracing.c:186-214
  *   calculateRayCollision raytracing.c:216-240
  *   calcColor            raytracing.c:262-296
+ *   calcDebugColor       raytracing.c:242-260 (RTC_F_DEBUG_BOUNCES)
  *   rowThread            main.c:81-104 (row-interleaved pthreads, main.c:84,285-302)
  *   vec3ToColor          raytracing.c:11-15 / moremath.c:25-30
  *
@@ -216,6 +217,24 @@ static vec3 o_calc_color(Ray ray, const OCtx *c, unsigned int *rng, unsigned lon
     return incomingLight;
 }
 
+/* calcDebugColor (raytracing.c:242-260): bounce count until the first miss, as grey */
+static vec3 o_calc_debug_color(Ray ray, const OCtx *c, unsigned int *rng, unsigned long long *segments)
+{
+    int i;
+    for (i = 0; i < c->maxBounce; ++i) {
+        OHit hit = o_collide(ray, c, segments);
+        if (hit.didHit) {
+            vec3 diffuseDir = o_normalized(o_plus(hit.normal, o_random_direction(rng)));
+            vec3 specularDir = o_reflect(ray.dir, hit.normal);
+            ray.dir = o_lerp(diffuseDir, specularDir, hit.mat.smoothness);
+            ray.pos = hit.hitPoint;
+        } else
+            break;
+    }
+    vec3 black = {0, 0, 0}, white = {1, 1, 1};
+    return o_lerp(black, white, i / (float)c->maxBounce);
+}
+
 /* ---- rowThread (main.c:81-104) -------------------------------------------------------------------- */
 typedef struct {
     const OCtx *ctx;
@@ -244,8 +263,11 @@ static void *o_row_thread(void *p)
             Ray ray = {a->cam->origin, dir};
             unsigned int rng = (unsigned int)(x + y * width);
             vec3 acc = {0, 0, 0};
-            for (int i = 0; i < d->spp; ++i)
-                acc = o_plus(acc, o_times(o_calc_color(ray, a->ctx, &rng, &a->segments), invSpp));
+            for (int i = 0; i < d->spp; ++i) {
+                vec3 c = (d->flags & RTC_F_DEBUG_BOUNCES) ? o_calc_debug_color(ray, a->ctx, &rng, &a->segments)
+                                                         : o_calc_color(ray, a->ctx, &rng, &a->segments);
+                acc = o_plus(acc, o_times(c, invSpp));
+            }
             size_t o = (size_t)r * (size_t)width + (size_t)x;
             if (a->out) {
                 a->out[o].r = o_float_to_uint(acc.x);
@@ -349,13 +371,13 @@ void oracle_random(const unsigned int *seeds, size_t n, int draws, float *unifor
 /* calcColor on explicit rays/seeds (tests compare with the reference's own calcColor via rtc_ref --kat-calc) */
 void oracle_calc_color(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                        const Scene *scene, int trianglesOnly, const Ray *rays, const unsigned int *seeds,
-                       const int *maxBounce, size_t n, vec3 *out, unsigned int *seedAfter)
+                       const int *maxBounce, size_t n, vec3 *out, unsigned int *seedAfter, int debug)
 {
     for (size_t i = 0; i < n; ++i) {
         OCtx ctx = {tris, triCount, spheres, sphereCount, scene, trianglesOnly, maxBounce[i]};
         unsigned int s = seeds[i];
         unsigned long long seg = 0;
-        out[i] = o_calc_color(rays[i], &ctx, &s, &seg);
+        out[i] = debug ? o_calc_debug_color(rays[i], &ctx, &s, &seg) : o_calc_color(rays[i], &ctx, &s, &seg);
         seedAfter[i] = s;
     }
 }

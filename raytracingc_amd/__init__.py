@@ -24,6 +24,7 @@ from ._abi import (  # noqa: F401
     CLI_PATH,
     LIB_PATH,
     RAY_DT,
+    RTC_F_DEBUG_BOUNCES,
     RTC_F_HOIST_PRIMARY,
     SCENE_DT,
     SPHERE_DT,
@@ -123,10 +124,14 @@ class RenderConfig:
     hoist: bool = False
     row_start: int = 0
     row_stride: int = 1
+    debug_bounces: bool = False  # calcDebugColor (raytracing.c:242-260) instead of calcColor
+
+    def flags(self) -> int:
+        return (RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
-                             self.row_start, self.row_stride, RTC_F_HOIST_PRIMARY if self.hoist else 0)
+                             self.row_start, self.row_stride, self.flags())
 
     def rows(self) -> int:
         d = self.desc()

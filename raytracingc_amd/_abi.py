@@ -74,6 +74,7 @@ class RtcStats(C.Structure):
 
 
 RTC_F_HOIST_PRIMARY = 0x1
+RTC_F_DEBUG_BOUNCES = 0x2
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
 assert C.sizeof(Vec3) == 12 and C.sizeof(Scene) == 56 and C.sizeof(Material) == 20

@@ -431,7 +431,7 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 #ifndef RTC_MIN_WAVES
 #define RTC_MIN_WAVES 1
 #endif
-template <bool SPHERES>
+template <bool SPHERES, bool DEBUG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_WAVES))) void rtc_render_kernel(
     RenderParams P)
 {
@@ -454,6 +454,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
 
     V3 acc{0.f, 0.f, 0.f};
     bool alive = valid && P.spp > 0 && P.maxBounce > 0;
+    if (DEBUG && valid && !(P.maxBounce > 0)) {
+        /* calcDebugColor with no bounce loop returns lerp(BLACK, WHITE, 0 / (float)maxBounce) */
+        const float t = 0.f / (float)P.maxBounce;
+        const V3 g = lerp(V3{0.f, 0.f, 0.f}, V3{1.f, 1.f, 1.f}, t);
+        for (int i = 0; i < P.spp; ++i)
+            acc = add(acc, mul(g, P.invSpp));
+    }
     int sample = 0, bounce = 0;
     V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
     unsigned segCalls = 0, segTraced = 0;
@@ -503,11 +510,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
                     emission = M.emission;
                     smoothness = M.smoothness;
                 }
-                /* calcColor hit branch, raytracing.c:274-287 */
+                /* calcColor hit branch, raytracing.c:274-287 (calcDebugColor :251-254 shares the first part) */
                 const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
                 const V3 specularDir = reflect(dir, normal);
                 dir = lerp(diffuseDir, specularDir, smoothness);
                 pos = hitPoint;
+                if (DEBUG) {
+                    bounce++;
+                    endSample = bounce >= P.maxBounce;
+                    if (endSample)
+                        light = lerp(V3{0.f, 0.f, 0.f}, V3{1.f, 1.f, 1.f}, (float)bounce / (float)P.maxBounce);
+                } else {
                 const V3 emitted = mul(color, emission);
                 light = add(light, mulv(emitted, rayColor));
                 rayColor = mulv(rayColor, color);
@@ -518,6 +531,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
                     bounce++;
                     endSample = bounce >= P.maxBounce;
                 }
+                }
+            } else if (DEBUG) {
+                /* calcDebugColor: first miss ends the sample with lerp(BLACK, WHITE, i / (float)maxBounce) */
+                light = lerp(V3{0.f, 0.f, 0.f}, V3{1.f, 1.f, 1.f}, (float)bounce / (float)P.maxBounce);
+                endSample = true;
             } else {
                 /* miss branch, raytracing.c:291 */
                 light = add(light, mulv(environment(dir, P.env), rayColor));
@@ -633,10 +651,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     if (s->triPadded > 0)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->prim,
                            s->triPadded, P.origin);
-    if (P.sphereCount > 0)
-        hipLaunchKernelGGL(rtc_render_kernel<true>, grid, dim3(kBlock), 0, st, P);
+    const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
+    if (P.sphereCount > 0 && debug)
+        hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, st, P);
+    else if (P.sphereCount > 0)
+        hipLaunchKernelGGL((rtc_render_kernel<true, false>), grid, dim3(kBlock), 0, st, P);
+    else if (debug)
+        hipLaunchKernelGGL((rtc_render_kernel<false, true>), grid, dim3(kBlock), 0, st, P);
     else
-        hipLaunchKernelGGL(rtc_render_kernel<false>, grid, dim3(kBlock), 0, st, P);
+        hipLaunchKernelGGL((rtc_render_kernel<false, false>), grid, dim3(kBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -12,6 +12,7 @@ the deterministic variant described in SURVEY.md F4 (oracle/ref_unity.c, oracle/
   kat_sphere.npz         raySphere
   kat_env.npz            getEnvironmentLight
   kat_calc_<scene>.npz   calcColor per (ray, seed, maxBounce)
+  kat_debug_<scene>.npz  calcDebugColor (raytracing.c:242-260) per (ray, seed, maxBounce)
   render_golden.json     full renders (main.c render loop): sha256 of the pre-quantisation float
                          framebuffer and md5 of the BMP, per configuration
 
@@ -260,7 +261,7 @@ def camera_rays(w, h, pixels):
     return rays
 
 
-def gen_kat_calc(work, rng, scene):
+def gen_kat_calc(work, rng, scene, debug=False):
     w, h = 480, 270
     # pixels where geometry is visible (rows 26-192 hold hits for the OBJ scenes)
     pix = [(int(x), int(y)) for x, y in zip(rng.integers(0, w, 600), rng.integers(20, 200, 600))]
@@ -280,10 +281,10 @@ def gen_kat_calc(work, rng, scene):
     kin["ray"], kin["seed"], kin["mb"] = rays, seeds, mb
     fi, fo = os.path.join(work, "calc.in"), os.path.join(work, "calc.out")
     kin.tofile(fi)
-    run_ref(["--kat-calc", mode_arg(scene), fi, fo], work)
+    run_ref(["--kat-debug" if debug else "--kat-calc", mode_arg(scene), fi, fo], work)
     out = np.fromfile(fo, np.dtype([("color", "<f4", 3), ("seedAfter", "<u4")]))
-    np.savez_compressed(os.path.join(HERE, f"kat_calc_{scene}.npz"), rays=rays, seeds=seeds, max_bounce=mb,
-                        color=out["color"], seed_after=out["seedAfter"])
+    np.savez_compressed(os.path.join(HERE, f"kat_{'debug' if debug else 'calc'}_{scene}.npz"), rays=rays, seeds=seeds,
+                        max_bounce=mb, color=out["color"], seed_after=out["seedAfter"])
 
 
 # (name, scene, W, H, spp, extra reference flags)
@@ -375,6 +376,8 @@ def main():
         gen_kat_env(work, rng)
         for s in ["ultracomplex", "default", "complex"]:
             gen_kat_calc(work, rng, s)
+        for s in ["ultracomplex", "default"]:
+            gen_kat_calc(work, rng, s, debug=True)
         gen_renders(work)
 
 

@@ -118,6 +118,22 @@ def test_hoisted_primary_is_bit_exact(name, gpu_available):
     assert s0["segments"] == s1["segments"]
 
 
+@pytest.mark.parametrize("scene,mb", [("default", 10), ("ultracomplex", 10), ("default", 3), ("fsuzane", 0)])
+def test_debug_bounce_integrator(scene, mb, gpu_available):
+    """calcDebugColor (raytracing.c:242-260) as a kernel variant (RTC_F_DEBUG_BOUNCES) == the oracle's, which
+    tests/test_oracle.py pins to the reference's own calcDebugColor."""
+    tris, tonly = load_tris(scene)
+    sph = scene_spheres(scene)
+    s, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(64, 36, 4, mb, bool(tonly), debug_bounces=True)
+    col, acc, st = rt.render(tris, sph, s, cam, cfg, want_accum=True)
+    d = RtcRenderDesc(64, 36, 4, mb, tonly, 0, 1, rt.RTC_F_DEBUG_BOUNCES)
+    ocol, oacc, oseg = orc.render(tris, sph, s, cam, d, threads=8)
+    mx, over, exact = _compare(acc, oacc)
+    assert over == 0 and st["segments"] == oseg and np.array_equal(col, ocol)
+    assert exact == 1.0  # no environment lookup in this integrator: bit-exact
+
+
 def test_row_partition_and_deinterleave(gpu_available):
     """Ranks render y = r + k*G into compact buffers; the gathered parts re-interleaved by the kernel equal
     the single-GPU frame bit for bit (G = 2..8 simulated on one device)."""

@@ -65,6 +65,18 @@ def test_calc_color_kat(scene):
     assert np.array_equal(after, k["seed_after"])
 
 
+@pytest.mark.parametrize("scene", ["ultracomplex", "default"])
+def test_calc_debug_color_kat(scene):
+    """calcDebugColor (raytracing.c:242-260), the bounce-count integrator (RTC_F_DEBUG_BOUNCES)."""
+    k = np.load(f"{GOLDEN}/kat_debug_{scene}.npz")
+    tris, tonly = load_tris(scene)
+    sc, _, _ = setup_from_flags({})
+    col, after = orc.calc_color(tris, scene_spheres(scene), sc, tonly, k["rays"], k["seeds"], k["max_bounce"],
+                                debug=True)
+    assert np.array_equal(_bits(col), _bits(k["color"]))
+    assert np.array_equal(after, k["seed_after"])
+
+
 GOLD = render_golden()
 
 
