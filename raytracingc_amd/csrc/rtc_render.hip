@@ -102,12 +102,22 @@ struct __attribute__((aligned(32))) DevMat {
 struct __attribute__((aligned(16))) DevSphere {
     float cx, cy, cz, radius, r, g, b, emission, smoothness, pad0, pad1, pad2;
 };
-/* Per-frame record for primary rays (bounce 0), whose origin is the camera for every pixel: the terms of
- * rayTriangle that depend only on the origin and the triangle -- s0 = origin - A, q0 = cross(s0, AB),
- * dAC0 = dot(AC, q0) (raytracing.c:198,202,206) -- are computed once per launch by rtc_prep_primary with the
- * same f32 operations, so the primary test stays bit-exact while skipping them.  64 B, scalar-loaded. */
-struct __attribute__((aligned(64))) DevPrim {
-    float nx, ny, nz, acx, acy, acz, abx, aby, abz, s0x, s0y, s0z, q0x, q0y, q0z, dac0;
+/* Per-launch records for primary rays (bounce 0): every primary ray starts at the camera origin O, so all
+ * the quantities rayTriangle derives from the ray are LINEAR in its direction d:
+ *   nd = d.N,  det = AB.(d x AC) = d.Gd,  uu = s0.(d x AC) = d.Gu,  vv = d.q0
+ * with s0 = O - A, q0 = s0 x AB, Gd = AC x AB, Gu = AC x s0 (raytracing.c:189-206).
+ * DevPrimF drives an exact-safe FILTER: FMA dot products against these vectors plus per-triangle error
+ * bounds (rtc_prep_primary derives them in double, see prim_bounds) reject a lane only when the
+ * reference's own float arithmetic provably rejects it.  Surviving lanes run the reference arithmetic with
+ * DevPrimX (s0, q0 and dot(AC, q0) computed once per launch with the reference's f32 ops: bit-exact). */
+struct __attribute__((aligned(64))) DevPrimF { /* 64 B: one s_load_dwordx16 */
+    float nx, ny, nz, mnd;     /* N and the |nd| margin */
+    float gdx, gdy, gdz, ed;   /* Gd and the |det| error bound */
+    float gux, guy, guz, m;    /* Gu and the combined edge margin */
+    float q0x, q0y, q0z, dac0; /* q0 (exact) and dot(AC, q0) (exact) */
+};
+struct __attribute__((aligned(64))) DevPrimX {
+    float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, pad[7];
 };
 
 struct RtcDeviceScene {
@@ -116,7 +126,8 @@ struct RtcDeviceScene {
     DevTri *tris;
     DevMat *mats;
     DevSphere *spheres;
-    DevPrim *prim; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
+    DevPrimF *primF; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
+    DevPrimX *primX;
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -197,7 +208,9 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     if (e == hipSuccess)
         e = hipMalloc(&s->spheres, ds.size() * sizeof(DevSphere));
     if (e == hipSuccess)
-        e = hipMalloc(&s->prim, dt.size() * sizeof(DevPrim));
+        e = hipMalloc(&s->primF, dt.size() * sizeof(DevPrimF));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->primX, dt.size() * sizeof(DevPrimX));
     if (e == hipSuccess)
         e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -225,8 +238,10 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->mats);
     if (s->spheres)
         (void)hipFree(s->spheres);
-    if (s->prim)
-        (void)hipFree(s->prim);
+    if (s->primF)
+        (void)hipFree(s->primF);
+    if (s->primX)
+        (void)hipFree(s->primX);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -245,7 +260,8 @@ struct RenderParams {
     const DevTri *__restrict__ tris;
     const DevMat *__restrict__ mats;
     const DevSphere *__restrict__ spheres;
-    const DevPrim *__restrict__ prim;
+    const DevPrimF *__restrict__ primF;
+    const DevPrimX *__restrict__ primX;
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced */
@@ -261,35 +277,63 @@ struct RenderParams {
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 
-/* rtc_prep_primary: per-launch primary-ray records (see DevPrim). */
-__global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict__ tris, DevPrim *__restrict__ prim,
-                                                        int triCount, V3 origin)
+/* Error bounds for the primary filter (u = 2^-24, |d_i| <= 1 + 2^-22 for a normalized float direction).
+ * Reference det: h = cross(d, AC) then a 3-term dot -> |det_e - d.(AC x AB)| <= 5.001 u |AB|_1 |AC|_1.
+ * Filter det: FMA dot with Gd rounded to float -> <= 4.004 u |AB|_1 |AC|_1.  Same with s0 for uu; vv uses q0
+ * (exact) on both sides (<= 6.002 u |q0|_1); nd uses N on both sides (<= 6.002 u |N|_1).  For u+v > 1 the
+ * filter forms w~ = (det~ - u~) - v~ (two more roundings, <= 2.0001 u (|det~| + |u~| + |v~|)) and the
+ * reference rejects once sigma*(det - uu - vv) < -2^-21 |det| (three roundings), so that edge carries the
+ * three bounds above, the subtraction error and 2^-21 |AB|_1 |AC|_1 (>= |det|).  Every bound is taken 4x and rounded up; the sign tests also carry 2^-60
+ * so a product that could round to -0 is never treated as negative. */
+__global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict__ tris, DevPrimF *__restrict__ pf,
+                                                        DevPrimX *__restrict__ px, int triCount, V3 origin)
 {
     const int t = blockIdx.x * 64 + threadIdx.x;
     if (t >= triCount)
         return;
     const DevTri T = tris[t];
-    const V3 AB{T.abx, T.aby, T.abz}, AC{T.acx, T.acy, T.acz};
+    const V3 AB{T.abx, T.aby, T.abz}, AC{T.acx, T.acy, T.acz}, N{T.nx, T.ny, T.nz};
     const V3 s0 = sub(origin, V3{T.ax, T.ay, T.az}); /* raytracing.c:198 */
     const V3 q0 = cross(s0, AB);                      /* :202 */
-    DevPrim r;
-    r.nx = T.nx;
-    r.ny = T.ny;
-    r.nz = T.nz;
-    r.acx = AC.x;
-    r.acy = AC.y;
-    r.acz = AC.z;
-    r.abx = AB.x;
-    r.aby = AB.y;
-    r.abz = AB.z;
-    r.s0x = s0.x;
-    r.s0y = s0.y;
-    r.s0z = s0.z;
-    r.q0x = q0.x;
-    r.q0y = q0.y;
-    r.q0z = q0.z;
-    r.dac0 = dot(AC, q0); /* :206 numerator */
-    prim[t] = r;
+    const float dac0 = dot(AC, q0);                   /* :206 numerator */
+    DevPrimX x;
+    x.abx = AB.x, x.aby = AB.y, x.abz = AB.z;
+    x.acx = AC.x, x.acy = AC.y, x.acz = AC.z;
+    x.s0x = s0.x, x.s0y = s0.y, x.s0z = s0.z;
+    for (int k = 0; k < 7; ++k)
+        x.pad[k] = 0.f;
+    px[t] = x;
+
+    /* exact-math direction vectors, in double, then rounded to float */
+    const double abx = AB.x, aby = AB.y, abz = AB.z, acx = AC.x, acy = AC.y, acz = AC.z;
+    const double sx = s0.x, sy = s0.y, sz = s0.z;
+    const double gdx = acy * abz - acz * aby, gdy = acz * abx - acx * abz, gdz = acx * aby - acy * abx;
+    const double gux = acy * sz - acz * sy, guy = acz * sx - acx * sz, guz = acx * sy - acy * sx;
+    auto n1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
+    const double u = 5.9604644775390625e-08; /* 2^-24 */
+    const double nAB = n1(abx, aby, abz), nAC = n1(acx, acy, acz), nS = n1(sx, sy, sz);
+    const double nQ = n1(q0.x, q0.y, q0.z), nN = n1(N.x, N.y, N.z);
+    const double eD = 9.006 * u * nAB * nAC;
+    const double eU = 9.006 * u * nS * nAC;
+    const double eV = 6.002 * u * nQ;
+    const double eW = eD + eU + eV + 2.0002 * u * (nAB * nAC + nS * nAC + nQ) + 4.8e-7 * nAB * nAC;
+    const double tiny = 8.673617379884035e-19; /* 2^-60 */
+    double m = fmax(fmax(eU, eV), eW) * 4.0 + tiny;
+    double ed = eD * 4.0;
+    double mnd = 6.002 * u * nN * 4.0;
+    /* gigantic or non-finite geometry: disable the filter for this triangle (always exact) */
+    const bool sane = ed < 2.5e-4 && nAB * nAC < 1e30 && nS * nAC < 1e30 && nQ < 1e30 && m < 1e30 && mnd < 1e30;
+    DevPrimF f;
+    f.nx = N.x, f.ny = N.y, f.nz = N.z;
+    f.gdx = (float)gdx, f.gdy = (float)gdy, f.gdz = (float)gdz;
+    f.gux = (float)gux, f.guy = (float)guy, f.guz = (float)guz;
+    f.q0x = q0.x, f.q0y = q0.y, f.q0z = q0.z;
+    f.dac0 = dac0;
+    /* margins rounded up to float */
+    f.mnd = sane ? __double2float_ru(mnd) : __builtin_inff();
+    f.ed = sane ? __double2float_ru(ed) : __builtin_inff();
+    f.m = sane ? __double2float_ru(m) : __builtin_inff();
+    pf[t] = f;
 }
 
 struct Closest {
@@ -314,39 +358,53 @@ __device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
 
 
 
-/* Primary segments (every live lane at bounce 0, pos == camera origin): rayTriangle with the per-launch
- * records.  A batch of kUnroll records is scalar-loaded at once (SGPR operands, no VGPR/LDS traffic); the
- * common path is two wave-uniform branches per triangle -- back face, then the exact-safe filter -- so the
- * scalar unit (exec-mask bookkeeping) does not become the limiter. */
+/* Primary segments (every live lane at bounce 0, pos == camera origin).
+ * Filter (per lane, ~20 VALU for a front-facing record, 4 for a back-facing one): FMA dot products of the
+ * direction with the DevPrimF vectors; sign-normalise u, v, w, dst by the sign of det (xor of the sign bit,
+ * exact); reject when the bounds prove the reference rejects:
+ *   nd > mnd                       => dot(dir, N) > 0            (raytracing.c:189)
+ *   |det~| + ed < 0.001           => |det| < EPSILON            (:195)
+ *   min(s*u~, s*v~, s*w~, s*dAC0) < -m => u < 0, v < 0, u+v > 1 or dst < 0   (:200-208)
+ * The exact reference arithmetic runs only for lanes the filter keeps (NaN directions are never kept:
+ * their det is NaN, so the reference cannot record a hit either).  Records are scalar-loaded in batches. */
+__device__ __forceinline__ float fdot(V3 d, float x, float y, float z) { return fmaf(d.z, z, fmaf(d.y, y, d.x * x)); }
+
 __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, Closest &c, int base)
 {
-    const int Tp = P.triPadded;
-    for (int t0 = 0; t0 < Tp; t0 += kUnroll) {
-        DevPrim RR[kUnroll];
+    const DevPrimF *rec = P.primF;
+    for (int t0 = 0; t0 < P.triPadded; t0 += kUnroll, rec += kUnroll) {
+        DevPrimF FF[kUnroll];
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
-            RR[k] = P.prim[t0 + k];
+            FF[k] = rec[k];
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k) {
-            const DevPrim &R = RR[k];
-            /* backface cull on the stored normal (raytracing.c:189) */
-            const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
-            if (!(nd >= 0.f)) {
-                const V3 h = cross(dir, V3{R.acx, R.acy, R.acz});
-                const float det = dot(V3{R.abx, R.aby, R.abz}, h);
-                const float uu = dot(V3{R.s0x, R.s0y, R.s0z}, h);
-                const float vv = dot(dir, V3{R.q0x, R.q0y, R.q0z});
-                const float r = __builtin_amdgcn_rcpf(det);
-                const bool detOk = !(-kEps < det && det < kEps);
-                if (detOk & maybe_hit(uu * r, vv * r, R.dac0 * r)) {
-                    /* the reference's arithmetic from here on (raytracing.c:197-208) */
-                    const float invDet = 1.f / det;
-                    const float u = uu * invDet;
-                    const float v = vv * invDet;
-                    const float dst = R.dac0 * invDet;
-                    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
-                        c.dst = dst;
-                        c.idx = base + t0 + k;
+            const DevPrimF &F = FF[k];
+            if (!(fdot(dir, F.nx, F.ny, F.nz) > F.mnd)) {
+                const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
+                const float ut = fdot(dir, F.gux, F.guy, F.guz);
+                const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
+                const float sg = copysignf(1.f, dt); /* exact sign normalisation (x * +-1) */
+                const float wt = (dt - ut) - vt;
+                const float mn = fminf(fminf(ut * sg, vt * sg), fminf(wt * sg, F.dac0 * sg));
+                if ((fabsf(dt) + F.ed >= 0.001f) & (mn + F.m >= 0.f)) {
+                    /* the reference's arithmetic (raytracing.c:189-208) */
+                    const int t = t0 + k;
+                    const DevPrimX X = P.primX[t];
+                    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
+                        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
+                        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
+                        if (!(-kEps < det && det < kEps)) {
+                            const float invDet = 1.f / det;
+                            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
+                            const float v = dot(dir, V3{F.q0x, F.q0y, F.q0z}) * invDet;
+                            const float dst = F.dac0 * invDet;
+                            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) &&
+                                dst < c.dst) {
+                                c.dst = dst;
+                                c.idx = base + t;
+                            }
+                        }
                     }
                 }
             }
@@ -647,10 +705,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.env = env_of(*scene);
     dim3 grid((d->width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
     hipStream_t st = (hipStream_t)stream;
-    P.prim = s->prim;
+    P.primF = s->primF;
+    P.primX = s->primX;
     if (s->triPadded > 0)
-        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->prim,
-                           s->triPadded, P.origin);
+        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->primF,
+                           s->primX, s->triPadded, P.origin);
     const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     if (P.sphereCount > 0 && debug)
         hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, st, P);
