@@ -87,10 +87,10 @@ extern "C" int rtc_device_count(int *count)
 
 /* ---- device scene layout ------------------------------------------------------------------------- */
 #ifndef RTC_UNROLL
-#define RTC_UNROLL 4
+#define RTC_UNROLL 2
 #endif
 constexpr int kUnroll = RTC_UNROLL; /* records per scalar-load batch; arrays are padded to a multiple of 8 */
-static_assert(8 % kUnroll == 0, "padding assumes kUnroll divides 8");
+static_assert(8 % (2 * kUnroll) == 0 || kUnroll == 1, "padding assumes two batches divide 8");
 /* 64 B per triangle, read wave-uniformly by s_load_dwordx16: A, AB, AC, N (the reference's stored normal). */
 struct __attribute__((aligned(64))) DevTri {
     float ax, ay, az, abx, aby, abz, acx, acy, acz, nx, ny, nz, pad0, pad1, pad2, pad3;
@@ -200,7 +200,7 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     RtcDeviceScene *s = new RtcDeviceScene();
     s->device = device;
     s->triCount = triCount;
-    s->triPadded = (triCount + kUnroll - 1) / kUnroll * kUnroll;
+    s->triPadded = (triCount + 7) / 8 * 8; /* whole pairs of batches; arrays hold 8 more records for prefetch */
     s->sphereCount = sphereCount;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
     if (e == hipSuccess)
@@ -369,46 +369,60 @@ __device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
  * their det is NaN, so the reference cannot record a hit either).  Records are scalar-loaded in batches. */
 __device__ __forceinline__ float fdot(V3 d, float x, float y, float z) { return fmaf(d.z, z, fmaf(d.y, y, d.x * x)); }
 
-__device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, Closest &c, int base)
+/* One primary record (see closest_primary). */
+__device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
+                                             Closest &c)
 {
-    const DevPrimF *rec = P.primF;
-    for (int t0 = 0; t0 < P.triPadded; t0 += kUnroll, rec += kUnroll) {
-        DevPrimF FF[kUnroll];
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k)
-            FF[k] = rec[k];
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            const DevPrimF &F = FF[k];
-            if (!(fdot(dir, F.nx, F.ny, F.nz) > F.mnd)) {
-                const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
-                const float ut = fdot(dir, F.gux, F.guy, F.guz);
-                const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
-                const float sg = copysignf(1.f, dt); /* exact sign normalisation (x * +-1) */
-                const float wt = (dt - ut) - vt;
-                const float mn = fminf(fminf(ut * sg, vt * sg), fminf(wt * sg, F.dac0 * sg));
-                if ((fabsf(dt) + F.ed >= 0.001f) & (mn + F.m >= 0.f)) {
-                    /* the reference's arithmetic (raytracing.c:189-208) */
-                    const int t = t0 + k;
-                    const DevPrimX X = P.primX[t];
-                    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
-                        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
-                        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
-                        if (!(-kEps < det && det < kEps)) {
-                            const float invDet = 1.f / det;
-                            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
-                            const float v = dot(dir, V3{F.q0x, F.q0y, F.q0z}) * invDet;
-                            const float dst = F.dac0 * invDet;
-                            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) &&
-                                dst < c.dst) {
-                                c.dst = dst;
-                                c.idx = base + t;
-                            }
-                        }
+    if (!(fdot(dir, F.nx, F.ny, F.nz) > F.mnd)) {
+        const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
+        const float ut = fdot(dir, F.gux, F.guy, F.guz);
+        const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
+        const float sg = copysignf(1.f, dt); /* exact sign normalisation (x * +-1) */
+        const float wt = (dt - ut) - vt;
+        const float mn = fminf(fminf(ut * sg, vt * sg), fminf(wt * sg, F.dac0 * sg));
+        if ((fabsf(dt) + F.ed >= 0.001f) & (mn + F.m >= 0.f)) {
+            /* the reference's arithmetic (raytracing.c:189-208) */
+            const DevPrimX X = P.primX[t];
+            if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
+                const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
+                const float det = dot(V3{X.abx, X.aby, X.abz}, h);
+                if (!(-kEps < det && det < kEps)) {
+                    const float invDet = 1.f / det;
+                    const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
+                    const float v = dot(dir, V3{F.q0x, F.q0y, F.q0z}) * invDet;
+                    const float dst = F.dac0 * invDet;
+                    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                        c.dst = dst;
+                        c.idx = base + t;
                     }
                 }
             }
         }
+    }
+}
+
+/* Records are scalar-loaded in two alternating batches of kUnroll: the next batch is in flight while the
+ * current one is tested (the arrays carry 8 spare records so the last prefetch stays in bounds). */
+__device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, Closest &c, int base)
+{
+    const DevPrimF *rec = P.primF;
+    DevPrimF A[kUnroll], B[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k)
+        A[k] = rec[k];
+    for (int t0 = 0; t0 < P.triPadded; t0 += 2 * kUnroll, rec += 2 * kUnroll) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            B[k] = rec[kUnroll + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            primary_test(P, dir, A[k], t0 + k, base, c);
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            A[k] = rec[2 * kUnroll + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
     }
 }
 
