@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "rtc_math.h"
+
 namespace rtcdev {
 
 struct V3 {
@@ -55,8 +57,8 @@ __device__ __forceinline__ float random_value(unsigned &s)
 __device__ __forceinline__ float random_normal(unsigned &s)
 {
     float theta = (float)(2 * 3.14159265 * (double)random_value(s));
-    float rho = (float)__builtin_sqrt(-2 * ::log((double)random_value(s)));
-    return (float)((double)rho * ::cos((double)theta));
+    float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)random_value(s)));
+    return (float)((double)rho * rtcmath::cos((double)theta));
 }
 /* RandomDiretion (moremath.c:104-108), components drawn x, y, z */
 __device__ __forceinline__ V3 random_direction(unsigned &s)
@@ -67,15 +69,10 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
     return normalized(V3{a, b, c});
 }
 
-/* powf for the environment (raytracing.c:153,155): evaluated in double and rounded once.  glibc's powf
- * is within 0.82 ulp, so the two differ by at most 1 ulp on a small fraction of arguments (covered by
- * the float tolerance; measured in tests/test_gpu_parity.py). */
-__device__ __forceinline__ float pow_ref(float x, float y)
-{
-    if (y == 0.f || x == 1.f)
-        return 1.f;
-    return (float)::exp2((double)y * ::log2((double)x));
-}
+/* powf for the environment (raytracing.c:153,155): evaluated in double and rounded once (rtc_math.h).
+ * glibc's powf is within 0.82 ulp, so the two differ by 1 ulp on a small fraction of arguments (covered
+ * by the float tolerance; tools/check_devmath.cpp counts them). */
+__device__ __forceinline__ float pow_ref(float x, float y) { return rtcmath::pow_ref(x, y); }
 
 struct EnvParams {
     V3 sun, horizon, zenith, ground;

@@ -86,6 +86,9 @@ extern "C" int rtc_device_count(int *count)
 }
 
 /* ---- device scene layout ------------------------------------------------------------------------- */
+#ifndef RTC_PF_ORDER
+#define RTC_PF_ORDER 0
+#endif
 #ifndef RTC_UNROLL
 #define RTC_UNROLL 2
 #endif
@@ -107,17 +110,22 @@ struct __attribute__((aligned(16))) DevSphere {
  *   nd = d.N,  det = AB.(d x AC) = d.Gd,  uu = s0.(d x AC) = d.Gu,  vv = d.q0
  * with s0 = O - A, q0 = s0 x AB, Gd = AC x AB, Gu = AC x s0 (raytracing.c:189-206).
  * DevPrimF drives an exact-safe FILTER: FMA dot products against these vectors plus per-triangle error
- * bounds (rtc_prep_primary derives them in double, see prim_bounds) reject a lane only when the
- * reference's own float arithmetic provably rejects it.  Surviving lanes run the reference arithmetic with
- * DevPrimX (s0, q0 and dot(AC, q0) computed once per launch with the reference's f32 ops: bit-exact). */
+ * bounds (rtc_prep_primary derives them in double) reject a lane only when the reference's own float
+ * arithmetic provably rejects it.  Surviving lanes run the reference arithmetic with DevPrimX (AB, AC, s0,
+ * q0 and dot(AC, q0) computed once per launch with the reference's f32 ops: bit-exact).
+ *
+ * Orientation folding: a hit needs dst = dot(AC, q0) * invDet >= EPSILON > 0, so sign(det) must equal the
+ * sign of dAC0 = dot(AC, q0) -- a per-triangle constant for primary rays.  The filter vectors are stored
+ * pre-multiplied by sigma = sign(dAC0) (exact negation), which turns the per-lane sign normalisation into
+ * nothing: a lane is a candidate iff  sigma*det~ >= c  and  min(sigma*u~, sigma*v~, sigma*w~) >= -m. */
 struct __attribute__((aligned(64))) DevPrimF { /* 64 B: one s_load_dwordx16 */
-    float nx, ny, nz, mnd;     /* N and the |nd| margin */
-    float gdx, gdy, gdz, ed;   /* Gd and the |det| error bound */
-    float gux, guy, guz, m;    /* Gu and the combined edge margin */
-    float q0x, q0y, q0z, dac0; /* q0 (exact) and dot(AC, q0) (exact) */
+    float nx, ny, nz, mnd;      /* N and the nd margin (-inf: the triangle can never be hit, skip it) */
+    float gdx, gdy, gdz, c;     /* sigma*Gd and the det threshold c = EPSILON - ed, rounded down */
+    float gux, guy, guz, negm;  /* sigma*Gu and -m (the combined edge margin, negated) */
+    float q0x, q0y, q0z, pad0;  /* sigma*q0 */
 };
 struct __attribute__((aligned(64))) DevPrimX {
-    float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, pad[7];
+    float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, q0x, q0y, q0z, dac0, pad[3];
 };
 
 struct RtcDeviceScene {
@@ -300,8 +308,9 @@ __global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict_
     x.abx = AB.x, x.aby = AB.y, x.abz = AB.z;
     x.acx = AC.x, x.acy = AC.y, x.acz = AC.z;
     x.s0x = s0.x, x.s0y = s0.y, x.s0z = s0.z;
-    for (int k = 0; k < 7; ++k)
-        x.pad[k] = 0.f;
+    x.q0x = q0.x, x.q0y = q0.y, x.q0z = q0.z;
+    x.dac0 = dac0;
+    x.pad[0] = x.pad[1] = x.pad[2] = 0.f;
     px[t] = x;
 
     /* exact-math direction vectors, in double, then rounded to float */
@@ -318,21 +327,26 @@ __global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict_
     const double eV = 6.002 * u * nQ;
     const double eW = eD + eU + eV + 2.0002 * u * (nAB * nAC + nS * nAC + nQ) + 4.8e-7 * nAB * nAC;
     const double tiny = 8.673617379884035e-19; /* 2^-60 */
-    double m = fmax(fmax(eU, eV), eW) * 4.0 + tiny;
-    double ed = eD * 4.0;
-    double mnd = 6.002 * u * nN * 4.0;
-    /* gigantic or non-finite geometry: disable the filter for this triangle (always exact) */
+    const double m = fmax(fmax(eU, eV), eW) * 4.0 + tiny;
+    const double ed = eD * 4.0;
+    const double mnd = 6.002 * u * nN * 4.0;
+    /* gigantic or non-finite geometry: disable the filter for this triangle (zero vectors and infinite
+     * margins: every finite direction is a candidate and the exact path decides) */
     const bool sane = ed < 2.5e-4 && nAB * nAC < 1e30 && nS * nAC < 1e30 && nQ < 1e30 && m < 1e30 && mnd < 1e30;
+    /* dAC0 == 0 (or NaN): dst is 0 or NaN for every ray, which the reference never records */
+    const bool never = !(dac0 < 0.f || dac0 > 0.f);
+    const float sg = dac0 < 0.f ? -1.f : 1.f;
     DevPrimF f;
     f.nx = N.x, f.ny = N.y, f.nz = N.z;
-    f.gdx = (float)gdx, f.gdy = (float)gdy, f.gdz = (float)gdz;
-    f.gux = (float)gux, f.guy = (float)guy, f.guz = (float)guz;
-    f.q0x = q0.x, f.q0y = q0.y, f.q0z = q0.z;
-    f.dac0 = dac0;
-    /* margins rounded up to float */
-    f.mnd = sane ? __double2float_ru(mnd) : __builtin_inff();
-    f.ed = sane ? __double2float_ru(ed) : __builtin_inff();
-    f.m = sane ? __double2float_ru(m) : __builtin_inff();
+    f.gdx = sane ? sg * (float)gdx : 0.f, f.gdy = sane ? sg * (float)gdy : 0.f, f.gdz = sane ? sg * (float)gdz : 0.f;
+    f.gux = sane ? sg * (float)gux : 0.f, f.guy = sane ? sg * (float)guy : 0.f, f.guz = sane ? sg * (float)guz : 0.f;
+    f.q0x = sane ? sg * q0.x : 0.f, f.q0y = sane ? sg * q0.y : 0.f, f.q0z = sane ? sg * q0.z : 0.f;
+    f.pad0 = 0.f;
+    /* margins rounded outwards to float: sigma*det >= 0.001f (float EPSILON compare, raytracing.c:195) and
+     * |det~ - det| <= ed give sigma*det~ >= 0.001f - ed >= c */
+    f.mnd = never ? -__builtin_inff() : (sane ? __double2float_ru(mnd) : __builtin_inff());
+    f.c = sane ? __double2float_rd((double)0.001f - ed) : -__builtin_inff();
+    f.negm = sane ? -__double2float_ru(m) : -__builtin_inff();
     pf[t] = f;
 }
 
@@ -359,12 +373,12 @@ __device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
 
 
 /* Primary segments (every live lane at bounce 0, pos == camera origin).
- * Filter (per lane, ~20 VALU for a front-facing record, 4 for a back-facing one): FMA dot products of the
- * direction with the DevPrimF vectors; sign-normalise u, v, w, dst by the sign of det (xor of the sign bit,
- * exact); reject when the bounds prove the reference rejects:
- *   nd > mnd                       => dot(dir, N) > 0            (raytracing.c:189)
- *   |det~| + ed < 0.001           => |det| < EPSILON            (:195)
- *   min(s*u~, s*v~, s*w~, s*dAC0) < -m => u < 0, v < 0, u+v > 1 or dst < 0   (:200-208)
+ * Filter (per lane, 13 VALU for a front-facing record, 4 for a back-facing one): FMA dot products of the
+ * direction with the orientation-folded DevPrimF vectors (sigma = sign(dAC0), see DevPrimF); reject when the
+ * bounds prove the reference rejects:
+ *   nd > mnd                        => dot(dir, N) > 0                          (raytracing.c:189)
+ *   sigma*det~ < c = EPSILON - ed   => |det| < EPSILON or sign(det) != sigma (then dst < 0)   (:195, :206)
+ *   min(sigma*u~, sigma*v~, sigma*w~) < -m => u < 0, v < 0 or u+v > 1       (:200-204)
  * The exact reference arithmetic runs only for lanes the filter keeps (NaN directions are never kept:
  * their det is NaN, so the reference cannot record a hit either).  Records are scalar-loaded in batches. */
 __device__ __forceinline__ float fdot(V3 d, float x, float y, float z) { return fmaf(d.z, z, fmaf(d.y, y, d.x * x)); }
@@ -377,10 +391,8 @@ __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, cons
         const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
         const float ut = fdot(dir, F.gux, F.guy, F.guz);
         const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
-        const float sg = copysignf(1.f, dt); /* exact sign normalisation (x * +-1) */
         const float wt = (dt - ut) - vt;
-        const float mn = fminf(fminf(ut * sg, vt * sg), fminf(wt * sg, F.dac0 * sg));
-        if ((fabsf(dt) + F.ed >= 0.001f) & (mn + F.m >= 0.f)) {
+        if ((dt >= F.c) & (fminf(fminf(ut, vt), wt) >= F.negm)) {
             /* the reference's arithmetic (raytracing.c:189-208) */
             const DevPrimX X = P.primX[t];
             if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
@@ -389,8 +401,8 @@ __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, cons
                 if (!(-kEps < det && det < kEps)) {
                     const float invDet = 1.f / det;
                     const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
-                    const float v = dot(dir, V3{F.q0x, F.q0y, F.q0z}) * invDet;
-                    const float dst = F.dac0 * invDet;
+                    const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
+                    const float dst = X.dac0 * invDet;
                     if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
                         c.dst = dst;
                         c.idx = base + t;
@@ -411,6 +423,24 @@ __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, C
     for (int k = 0; k < kUnroll; ++k)
         A[k] = rec[k];
     for (int t0 = 0; t0 < P.triPadded; t0 += 2 * kUnroll, rec += 2 * kUnroll) {
+#if RTC_PF_ORDER
+        /* SMEM returns out of order, so the first use of a batch waits for every scalar load in flight:
+         * issue the next batch only after the current batch has been touched */
+        primary_test(P, dir, A[0], t0, base, c);
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            B[k] = rec[kUnroll + k];
+#pragma unroll
+        for (int k = 1; k < kUnroll; ++k)
+            primary_test(P, dir, A[k], t0 + k, base, c);
+        primary_test(P, dir, B[0], t0 + kUnroll, base, c);
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            A[k] = rec[2 * kUnroll + k];
+#pragma unroll
+        for (int k = 1; k < kUnroll; ++k)
+            primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
+#else
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
             B[k] = rec[kUnroll + k];
@@ -423,6 +453,7 @@ __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, C
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
             primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
+#endif
     }
 }
 

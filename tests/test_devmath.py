@@ -1,0 +1,41 @@
+"""The compact double-precision log / cos / exp2 the device uses (raytracingc_amd/csrc/rtc_math.h) against
+glibc, on the input sets the renderer produces: every float u in (0, 1] for Box-Muller's log (moremath.c:100),
+every float theta in [0, 2*pi] for its cos (moremath.c:101), every float x in [0, 1] for powf (raytracing.c:153,
+155).  The header is the same source the HIP kernel compiles (host and device share IEEE double arithmetic,
+with explicit fma and -ffp-contract=off), so what matters -- the FLOAT results the reference derives -- is
+checked here on the CPU.  This test samples every 251st float; `tools/check_devmath.cpp` with stride 1 is the
+exhaustive run (recorded in DESIGN.md: 0 float mismatches for log and cos over 1.07e9 / 1.09e9 inputs)."""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("devmath") / "check_devmath")
+    src = os.path.join(REPO, "tools", "check_devmath.cpp")
+    r = subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fopenmp", "-std=c++17", src, "-o", exe],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip(f"g++ unavailable or failed: {r.stderr[-300:]}")
+    return exe
+
+
+def test_devmath_matches_glibc_where_it_matters(checker):
+    out = subprocess.run([checker, "251"], capture_output=True, text=True, timeout=300).stdout
+    m = re.search(r"log: (\d+) inputs, (\d+) double != glibc, (\d+) float rho", out)
+    assert m and int(m.group(1)) > 4_000_000 and int(m.group(3)) == 0, out
+    m = re.search(r"cos: (\d+) inputs, (\d+) double != glibc, (\d+) float rho\*cos", out)
+    assert m and int(m.group(3)) == 0, out
+    for y in ("0.35", "22", "7.5"):
+        m = re.search(rf"pow y={y}: (\d+) inputs, (\d+) != glibc powf, (\d+) != double-glibc", out)
+        assert m, out
+        n, vs_glibc, vs_cr = map(int, m.groups())
+        assert vs_cr <= n * 1e-7  # same correctly-rounded result as the double-glibc evaluation
+        assert vs_glibc <= n * 1e-3  # glibc powf itself is within 0.82 ulp, not correctly rounded

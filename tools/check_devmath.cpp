@@ -1,0 +1,65 @@
+// Exhaustive check of raytracingc_amd/csrc/rtc_math.h against glibc on the input sets the renderer produces.
+//   g++ -O2 -ffp-contract=off -fopenmp -std=c++17 tools/check_devmath.cpp -o /tmp/check_devmath
+//   /tmp/check_devmath [stride]      (stride 1 = every float; larger = sampled)
+// Reports, per function, how many inputs give a different double / a different float result than glibc.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../raytracingc_amd/csrc/rtc_math.h"
+
+static float f_of(uint32_t b)
+{
+    float f;
+    memcpy(&f, &b, 4);
+    return f;
+}
+
+int main(int argc, char **argv)
+{
+    const uint32_t stride = argc > 1 ? (uint32_t)atoi(argv[1]) : 1;
+    // 1. log of u in (0, 1] -> rho = (float)sqrt(-2 log u)   (moremath.c:100)
+    long long n1 = 0, dlog = 0, drho = 0;
+#pragma omp parallel for reduction(+ : n1, dlog, drho) schedule(static, 65536)
+    for (long long b = 1; b <= 0x3f800000LL; b += stride) {
+        const double u = (double)f_of((uint32_t)b);
+        const double a = rtcmath::log(u), g = ::log(u);
+        n1++;
+        dlog += (a != g);
+        drho += ((float)sqrt(-2 * a) != (float)sqrt(-2 * g));
+    }
+    printf("log: %lld inputs, %lld double != glibc, %lld float rho != glibc\n", n1, dlog, drho);
+    // 2. cos of theta in [0, 2*pi) as a float (moremath.c:99-101)
+    long long n2 = 0, dcos = 0, dprod = 0;
+#pragma omp parallel for reduction(+ : n2, dcos, dprod) schedule(static, 65536)
+    for (long long b = 0; b <= 0x40c90fdbLL; b += stride) {
+        const double t = (double)f_of((uint32_t)b);
+        const double a = rtcmath::cos(t), g = ::cos(t);
+        n2++;
+        dcos += (a != g);
+        // a product with a few typical rho values
+        const float rhos[4] = {0.37f, 1.0f, 1.7724539f, 3.3f};
+        for (float r : rhos)
+            dprod += ((float)((double)r * a) != (float)((double)r * g));
+    }
+    printf("cos: %lld inputs, %lld double != glibc, %lld float rho*cos != glibc (4 rho each)\n", n2, dcos, dprod);
+    // 3. powf(x, y) for x in [0, 1] (raytracing.c:153,155)
+    const float ys[3] = {0.35f, 22.f, 7.5f};
+    for (float y : ys) {
+        long long n3 = 0, dglibc = 0, dcr = 0;
+#pragma omp parallel for reduction(+ : n3, dglibc, dcr) schedule(static, 65536)
+        for (long long b = 0; b <= 0x3f800000LL; b += stride) {
+            const float x = f_of((uint32_t)b);
+            const float a = rtcmath::pow_ref(x, y);
+            const float g = powf(x, y);
+            const float c = (y == 0.f || x == 1.f) ? 1.f : (float)::exp2((double)y * ::log2((double)x));
+            n3++;
+            dglibc += (a != g);
+            dcr += (a != c);
+        }
+        printf("pow y=%g: %lld inputs, %lld != glibc powf, %lld != double-glibc exp2(y*log2 x)\n", y, n3, dglibc, dcr);
+    }
+    return 0;
+}
