@@ -104,10 +104,10 @@ def main():
     scene = rt.default_scene()
     cam = rt.camera_basis()
     ds = rt.DeviceScene(tris, None, device=local)
-    seg = torch.zeros(2, dtype=torch.int64, device=dev)
+    seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device=dev)
 
-    def make(hoist):
-        cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist)
+    def make(hoist, tile_cull=True):
+        cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist, tile_cull=tile_cull)
         return FrameRenderer(cfg, hip_part_renderer(ds, scene, cam, seg), dev)
 
     def run(fr, steps, warmup):
@@ -150,18 +150,25 @@ def main():
         return float(t[0]), float(t[1]), [int(v) // steps for v in segs.tolist()]
 
     fr = make(False)
-    t, kern_ms, (seg_calls, seg_traced) = run(fr, args.steps, args.warmup)
+    t, kern_ms, (seg_calls, seg_traced, tri_tests, _) = run(fr, args.steps, args.warmup)
     samples = W * H * spp
     value = samples * args.steps / t / 1e6
     frame = fr.frame.clone() if rank == 0 else None
 
-    hoisted = None
+    hoisted = brute = None
     if not args.no_hoisted:
         frh = make(True)
-        th, kh, (hc, ht) = run(frh, args.steps, 1)
-        hoisted = {"value": samples * args.steps / th / 1e6, "ms_per_step": th / args.steps * 1e3,
-                   "kernel_ms": kh, "segments_traced": ht,
+        th, kh, (hc, ht, htests, _) = run(frh, args.steps, 1)
+        hoisted = {"value": round(samples * args.steps / th / 1e6, 3), "ms_per_step": round(th / args.steps * 1e3, 4),
+                   "kernel_ms": round(kh, 4), "segments_traced": ht, "tri_tests": htests,
                    "bit_exact_vs_faithful": bool(rank != 0 or torch.equal(frh.frame, frame))}
+        # the same faithful frame without the tile candidate lists (every primary segment tests every
+        # triangle, as calculateRayCollision does): for comparison only
+        frb = make(False, tile_cull=False)
+        tb, kb, (bc, bt, btests, _) = run(frb, max(2, args.steps // 2), 1)
+        brute = {"value": round(samples * max(2, args.steps // 2) / tb / 1e6, 3),
+                 "ms_per_step": round(tb / max(2, args.steps // 2) * 1e3, 4), "kernel_ms": round(kb, 4),
+                 "tri_tests": btests, "bit_exact_vs_culled": bool(rank != 0 or torch.equal(frb.frame, frame))}
 
     if rank == 0:
         # D2H of the finished frame, reported separately (never `value`)
@@ -170,10 +177,14 @@ def main():
         host = frame.cpu()
         d2h_ms = (time.perf_counter() - t0) * 1e3
         T = len(tris)
-        tests = seg_traced * T  # ray-triangle tests per frame, all ranks (traced closest-hit queries x T)
+        # ray-triangle tests the kernel evaluated per frame, all ranks (device counter: each traced segment x
+        # the triangles it visits -- its tile's candidates for a primary segment, all T otherwise)
+        tests = tri_tests
         # per launch on one GPU: this rank's share of the tests; kernel time = mean of its launches
         tests_per_launch = tests / world
         achieved_tf = tests_per_launch * FLOPS_PER_TEST / (kern_ms * 1e-3) / 1e12
+        # SURVEY §8(d)'s brute-force count (traced segments x T x 57): the work calculateRayCollision does
+        bf_tf = seg_traced / world * T * FLOPS_PER_TEST / (kern_ms * 1e-3) / 1e12
         scene_bytes = T * 68
         out_bytes = fr.rows * W * 3
         alg_bytes = scene_bytes + out_bytes
@@ -202,21 +213,26 @@ def main():
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
-                       "mode": "faithful (every sample re-traces its primary ray)"},
+                       "mode": "faithful (every sample re-traces its primary ray, over its 8x8 tile's candidate triangles)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
                          "kernel": "rtc_render_kernel", "kernel_ms": round(kern_ms, 4),
                          "work_per_launch": f"{tests_per_launch:.4g} ray-triangle tests x {FLOPS_PER_TEST} flop",
                          "hbm_achieved_gbs": round(alg_bytes / (kern_ms * 1e-3) / 1e9, 3),
-                         "hbm_peak_gbs": HBM_PEAK_GBS},
+                         "hbm_peak_gbs": HBM_PEAK_GBS,
+                         "bruteforce_equiv_tflops": round(bf_tf, 3),
+                         "note": "achieved counts the tests evaluated; bruteforce_equiv counts segments x T "
+                                 "(the reference's brute-force work) over the same time"},
             "frame_ms": round(t / args.steps * 1e3, 4),
             "segments_per_frame": seg_calls,
             "segments_traced_per_frame": seg_traced,
             "msegments_per_s": round(seg_traced * args.steps / t / 1e6, 2),
+            "tri_tests_per_frame": tests,
             "gtests_per_s": round(tests * args.steps / t / 1e9, 2),
             "d2h_ms": round(d2h_ms, 3),
             "hoisted": hoisted,
+            "no_tile_cull": brute,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb, ccol = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_row_stride)

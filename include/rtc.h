@@ -55,12 +55,15 @@ typedef struct RtcRenderDesc {
 
 #define RTC_F_HOIST_PRIMARY 0x1  /* bit-exact: trace each pixel's primary ray once; default off */
 #define RTC_F_DEBUG_BOUNCES 0x2  /* calcDebugColor (raytracing.c:242-260) instead of calcColor: bounce-count grey */
+#define RTC_F_NO_TILE_CULL  0x4  /* primary segments test every triangle (brute force, as calculateRayCollision
+                                    does) instead of the 8x8 tile's candidate list; same output bit for bit */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */
     double totalMs;              /* wall time of the whole rtc_render call incl. uploads / D2H */
     unsigned long long segments; /* closest-hit queries traced (calculateRayCollision calls) */
     unsigned long long samples;  /* camera samples = pixels * spp */
+    unsigned long long triTests; /* ray-triangle tests evaluated (segments x triangles the segment visits) */
 } RtcStats;
 
 /* ---- error codes ----------------------------------------------------------------------------------- */
@@ -120,8 +123,12 @@ int rtc_scene_release(RtcDeviceScene *s);
 int rtc_rows_selected(const RtcRenderDesc *d);
 /* Asynchronous on `stream` (a hipStream_t, NULL = default stream).  dColors: device buffer of
  * rows_selected*width*3 bytes; dAccum: nullable device float buffer rows_selected*width*3; dSegments:
- * nullable device u64[2] the kernel atomically adds to: [0] calculateRayCollision calls (the reference's
- * segment count), [1] closest-hit queries actually traced (smaller with RTC_F_HOIST_PRIMARY). */
+ * nullable device u64[RTC_SEGMENT_COUNTERS] the kernel atomically adds to: [0] calculateRayCollision calls
+ * (the reference's segment count), [1] closest-hit queries actually traced (smaller with
+ * RTC_F_HOIST_PRIMARY), [2] ray-triangle tests evaluated, [3] reserved.
+ * A scene handle serves one stream at a time: its per-launch scratch (primary-ray records, tile candidate
+ * lists) is rewritten by every launch. */
+#define RTC_SEGMENT_COUNTERS 4
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,
                           unsigned long long *dSegments, void *stream);

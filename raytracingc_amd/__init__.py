@@ -26,6 +26,8 @@ from ._abi import (  # noqa: F401
     RAY_DT,
     RTC_F_DEBUG_BOUNCES,
     RTC_F_HOIST_PRIMARY,
+    RTC_F_NO_TILE_CULL,
+    RTC_SEGMENT_COUNTERS,
     SCENE_DT,
     SPHERE_DT,
     TRIANGLE_DT,
@@ -125,9 +127,11 @@ class RenderConfig:
     row_start: int = 0
     row_stride: int = 1
     debug_bounces: bool = False  # calcDebugColor (raytracing.c:242-260) instead of calcColor
+    tile_cull: bool = True  # primary segments visit their 8x8 tile's candidate triangles (bit-exact)
 
     def flags(self) -> int:
-        return (RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
+        return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
+                | (0 if self.tile_cull else RTC_F_NO_TILE_CULL))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
@@ -159,7 +163,7 @@ def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, devic
     check(lib().rtc_render(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), device,
                            _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render")
     return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples}
+                           "samples": st.samples, "tri_tests": st.triTests}
 
 
 def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, num_devices: int,
@@ -174,7 +178,7 @@ def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig,
     check(lib().rtc_render_multi(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), num_devices,
                                  _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render_multi")
     return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples}
+                           "samples": st.samples, "tri_tests": st.triTests}
 
 
 class DeviceScene:

@@ -70,11 +70,14 @@ class RtcStats(C.Structure):
         ("totalMs", C.c_double),
         ("segments", C.c_ulonglong),
         ("samples", C.c_ulonglong),
+        ("triTests", C.c_ulonglong),
     ]
 
 
 RTC_F_HOIST_PRIMARY = 0x1
 RTC_F_DEBUG_BOUNCES = 0x2
+RTC_F_NO_TILE_CULL = 0x4
+RTC_SEGMENT_COUNTERS = 4  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
 assert C.sizeof(Vec3) == 12 and C.sizeof(Scene) == 56 and C.sizeof(Material) == 20

@@ -136,6 +136,10 @@ struct RtcDeviceScene {
     DevSphere *spheres;
     DevPrimF *primF; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
     DevPrimX *primX;
+    /* per-launch scratch, written by rtc_tile_cull: one candidate bit-set of maskWords u64 per 8x8 tile */
+    unsigned long long *tileMask;
+    size_t tileMaskCap; /* capacity, u64 words */
+    int maskWords;      /* ceil(triPadded / 64) */
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -210,6 +214,7 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     s->triCount = triCount;
     s->triPadded = (triCount + 7) / 8 * 8; /* whole pairs of batches; arrays hold 8 more records for prefetch */
     s->sphereCount = sphereCount;
+    s->maskWords = (s->triPadded + 63) / 64;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
     if (e == hipSuccess)
         e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
@@ -250,6 +255,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->primF);
     if (s->primX)
         (void)hipFree(s->primX);
+    if (s->tileMask)
+        (void)hipFree(s->tileMask);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -270,10 +277,11 @@ struct RenderParams {
     const DevSphere *__restrict__ spheres;
     const DevPrimF *__restrict__ primF;
     const DevPrimX *__restrict__ primX;
+    const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
-    unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced */
-    int triCount, triPadded, sphereCount;
+    unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
+    int triCount, triPadded, sphereCount, maskWords;
     int width, height, rows, rowStart, rowStride;
     int spp, maxBounce;
     int hoist;
@@ -284,6 +292,37 @@ struct RenderParams {
 };
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
+
+/* The pixel a lane renders and its primary ray (rowThread, main.c:88-94).  A 256-thread workgroup covers
+ * 16x16 pixels of the launch's rows; wave w of it the 8x8 tile (w & 1, w >> 1). */
+struct PixelRay {
+    int x, r, y;
+    bool valid;
+    V3 dir;
+};
+
+__device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P)
+{
+    PixelRay px;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    px.x = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
+    px.r = blockIdx.y * kTileH + (wave >> 1) * 8 + (lane >> 3);
+    px.valid = px.x < P.width && px.r < P.rows;
+    px.y = P.rowStart + px.r * P.rowStride;
+    /* integer halves, then int->float, f32 divide */
+    const float dx = (float)(px.x - P.width / 2) / (float)(P.height / 2);
+    const float dy = (float)(px.y - P.height / 2) / (float)(P.height / 2);
+    px.dir = normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
+    return px;
+}
+
+/* This wave's 8x8 tile in the launch (made provably wave-uniform, so tile data is scalar-loaded). */
+__device__ __forceinline__ int wave_tile()
+{
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return (blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1);
+}
 
 /* Error bounds for the primary filter (u = 2^-24, |d_i| <= 1 + 2^-22 for a normalized float direction).
  * Reference det: h = cross(d, AC) then a 3-term dot -> |det_e - d.(AC x AB)| <= 5.001 u |AB|_1 |AC|_1.
@@ -380,19 +419,30 @@ __device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
  *   sigma*det~ < c = EPSILON - ed   => |det| < EPSILON or sign(det) != sigma (then dst < 0)   (:195, :206)
  *   min(sigma*u~, sigma*v~, sigma*w~) < -m => u < 0, v < 0 or u+v > 1       (:200-204)
  * The exact reference arithmetic runs only for lanes the filter keeps (NaN directions are never kept:
- * their det is NaN, so the reference cannot record a hit either).  Records are scalar-loaded in batches. */
+ * their det is NaN, so the reference cannot record a hit either).  Records are scalar-loaded in batches.
+ * prim_backfacing / prim_pass are THE filter: the render kernel and rtc_tile_cull both use them. */
 __device__ __forceinline__ float fdot(V3 d, float x, float y, float z) { return fmaf(d.z, z, fmaf(d.y, y, d.x * x)); }
+
+__device__ __forceinline__ bool prim_backfacing(V3 dir, const DevPrimF &F)
+{
+    return fdot(dir, F.nx, F.ny, F.nz) > F.mnd;
+}
+
+__device__ __forceinline__ bool prim_pass(V3 dir, const DevPrimF &F)
+{
+    const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
+    const float ut = fdot(dir, F.gux, F.guy, F.guz);
+    const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
+    const float wt = (dt - ut) - vt;
+    return (dt >= F.c) & (fminf(fminf(ut, vt), wt) >= F.negm);
+}
 
 /* One primary record (see closest_primary). */
 __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
                                              Closest &c)
 {
-    if (!(fdot(dir, F.nx, F.ny, F.nz) > F.mnd)) {
-        const float dt = fdot(dir, F.gdx, F.gdy, F.gdz);
-        const float ut = fdot(dir, F.gux, F.guy, F.guz);
-        const float vt = fdot(dir, F.q0x, F.q0y, F.q0z);
-        const float wt = (dt - ut) - vt;
-        if ((dt >= F.c) & (fminf(fminf(ut, vt), wt) >= F.negm)) {
+    if (!prim_backfacing(dir, F)) {
+        if (prim_pass(dir, F)) {
             /* the reference's arithmetic (raytracing.c:189-208) */
             const DevPrimX X = P.primX[t];
             if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
@@ -413,8 +463,9 @@ __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, cons
     }
 }
 
-/* Records are scalar-loaded in two alternating batches of kUnroll: the next batch is in flight while the
- * current one is tested (the arrays carry 8 spare records so the last prefetch stays in bounds). */
+/* Brute force over every record (RTC_F_NO_TILE_CULL).  Records are scalar-loaded in two alternating
+ * batches of kUnroll: the next batch is in flight while the current one is tested (the arrays carry 8 spare
+ * records so the last prefetch stays in bounds). */
 __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, Closest &c, int base)
 {
     const DevPrimF *rec = P.primF;
@@ -454,6 +505,22 @@ __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, C
         for (int k = 0; k < kUnroll; ++k)
             primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
 #endif
+    }
+}
+
+/* Only the tile's candidates (rtc_tile_cull), in ascending index order, so ties keep the lowest index as
+ * calculateRayCollision's strict `<` does (raytracing.c:231).  `mask` is wave-uniform: the bit-set words
+ * and the records are scalar loads. */
+__device__ __forceinline__ void closest_primary_listed(const RenderParams &P, V3 dir, Closest &c, int base,
+                                                       const unsigned long long *__restrict__ mask)
+{
+    for (int w = 0; w < P.maskWords; ++w) {
+        unsigned long long m = mask[w];
+        while (m) {
+            const int t = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            primary_test(P, dir, P.primF[t], t, base, c);
+        }
     }
 }
 
@@ -498,9 +565,11 @@ __device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V
 /* calculateRayCollision (raytracing.c:216-240): spheres first (only if !trianglesOnly), then triangles
  * in index order; a candidate replaces the current one only if strictly closer (ties keep the lower
  * index).  The loop trip counts are kernel arguments, so the triangle index is wave-uniform and its
- * record is fetched with scalar loads.  `primaryWave` (wave-uniform) = every live lane is at bounce 0. */
+ * record is fetched with scalar loads.  `primaryWave` (wave-uniform) = every live lane is at bounce 0;
+ * `mask` (wave-uniform, nullable) = the tile's primary candidates. */
 template <bool SPHERES>
-__device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir, bool primaryWave)
+__device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir, bool primaryWave,
+                                               const unsigned long long *mask)
 {
     Closest c{999999.f, -1};
     if (SPHERES) {
@@ -514,11 +583,42 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
         }
     }
     const int base = SPHERES ? P.sphereCount : 0;
-    if (primaryWave)
-        closest_primary(P, dir, c, base);
-    else
+    if (primaryWave) {
+        if (mask)
+            closest_primary_listed(P, dir, c, base, mask);
+        else
+            closest_primary(P, dir, c, base);
+    } else {
         closest_general(P, pos, dir, c, base);
+    }
     return c;
+}
+
+/* Tile candidate lists for primary segments.  A pixel's primary ray is the same ray for every sample
+ * (main.c:88-94: no jitter), so the primary filter's verdict for (pixel, triangle) is the same for
+ * every sample.  One pass over the launch's pixels records, per 8x8 tile (= one wave of the render kernel),
+ * the set of triangles the filter keeps for at least one pixel of the tile; the render kernel's primary
+ * segments then visit only that set, in index order.  A triangle left out fails the filter for every pixel
+ * of the tile, so the reference's rayTriangle rejects it for every primary ray there: the closest hit is
+ * unchanged, bit for bit.  The filter is the render kernel's own (prim_backfacing / prim_pass, same records,
+ * same pixel_ray). */
+__global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask)
+{
+    const PixelRay px = pixel_ray(P);
+    const int lane = threadIdx.x & 63;
+    unsigned long long *out = mask + (size_t)wave_tile() * P.maskWords;
+    for (int w = 0; w < P.maskWords; ++w) {
+        unsigned long long bits = 0;
+        const int n = min(64, P.triPadded - w * 64);
+        for (int k = 0; k < n; ++k) {
+            const DevPrimF F = P.primF[w * 64 + k];
+            const bool keep = px.valid && !prim_backfacing(px.dir, F) && prim_pass(px.dir, F);
+            if (__any(keep))
+                bits |= 1ull << k;
+        }
+        if (lane == 0)
+            out[w] = bits;
+    }
 }
 
 #ifdef RTC_DIAG
@@ -543,17 +643,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     unsigned diagIters = 0;
 #endif
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
-    const int r = blockIdx.y * kTileH + (wave >> 1) * 8 + (lane >> 3);
-    const bool valid = x < P.width && r < P.rows;
-    const int y = P.rowStart + r * P.rowStride;
-
-    /* rowThread primary ray (main.c:88-94): integer halves, then int->float, f32 divide */
-    const float dx = (float)(x - P.width / 2) / (float)(P.height / 2);
-    const float dy = (float)(y - P.height / 2) / (float)(P.height / 2);
-    const V3 pdir = normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
+    const PixelRay px = pixel_ray(P);
+    const int x = px.x, r = px.r, y = px.y;
+    const bool valid = px.valid;
+    const V3 pdir = px.dir;
     unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
+
+    /* this wave's primary candidates (rtc_tile_cull) */
+    const unsigned long long *tmask = nullptr;
+    unsigned listLen = (unsigned)P.triCount;
+    if (P.tileMask) {
+        tmask = P.tileMask + (size_t)wave_tile() * P.maskWords;
+        listLen = 0;
+        for (int w = 0; w < P.maskWords; ++w)
+            listLen += (unsigned)__popcll(tmask[w]);
+    }
 
     V3 acc{0.f, 0.f, 0.f};
     bool alive = valid && P.spp > 0 && P.maxBounce > 0;
@@ -567,13 +671,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     int sample = 0, bounce = 0;
     V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
     unsigned segCalls = 0, segTraced = 0;
+    unsigned long long segTests = 0;
 
     /* bit-exact primary-hit hoisting: the primary ray consumes no RNG, so its closest hit
      * is a function of the pixel; trace it once instead of once per sample. */
     Closest primary{999999.f, -1};
     if (P.hoist && alive) {
-        primary = closest_hit<SPHERES>(P, pos, dir, true);
+        primary = closest_hit<SPHERES>(P, pos, dir, true, tmask);
         segTraced++;
+        segTests += listLen;
     }
 
     while (__any(alive)) {
@@ -589,8 +695,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
             if (!needTrace) {
                 c = primary;
             } else {
-                c = closest_hit<SPHERES>(P, pos, dir, primaryWave);
+                c = closest_hit<SPHERES>(P, pos, dir, primaryWave, tmask);
                 segTraced++;
+                segTests += primaryWave ? listLen : (unsigned)P.triCount;
             }
             bool endSample;
             if (c.idx >= 0) {
@@ -675,6 +782,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     }
 #ifdef RTC_DIAG
     if (g_rtc_diag && lane == 0) {
+        const int wave = threadIdx.x >> 6;
         const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
         g_rtc_diag[3 * w] = __builtin_amdgcn_s_memtime() - diagT0;
         g_rtc_diag[3 * w + 1] = diagIters;
@@ -682,14 +790,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     }
 #endif
     if (P.segments) {
-        unsigned long long a = segCalls, b = segTraced;
+        unsigned long long a = segCalls, b = segTraced, n = segTests;
         for (int off = 32; off > 0; off >>= 1) {
             a += __shfl_xor(a, off);
             b += __shfl_xor(b, off);
+            n += __shfl_xor(n, off);
         }
         if (lane == 0) {
             atomicAdd(&P.segments[0], a);
             atomicAdd(&P.segments[1], b);
+            atomicAdd(&P.segments[2], n);
         }
     }
 }
@@ -733,6 +843,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.triCount = s->triCount;
     P.triPadded = s->triPadded;
     P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
+    P.maskWords = s->maskWords;
     P.width = d->width;
     P.height = d->height;
     P.rows = rows;
@@ -752,9 +863,28 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     hipStream_t st = (hipStream_t)stream;
     P.primF = s->primF;
     P.primX = s->primX;
+    /* tile candidate lists: one bit-set per 8x8 tile (4 per workgroup), grown on demand (hipFree
+     * synchronises, so a previous launch still reading the old buffer has finished) */
+    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords > 0;
+    if (cull) {
+        const size_t need = (size_t)grid.x * 2 * grid.y * 2 * (size_t)s->maskWords;
+        if (need > s->tileMaskCap) {
+            RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
+            if (ms->tileMask)
+                HIP_TRY(hipFree(ms->tileMask));
+            ms->tileMask = nullptr;
+            ms->tileMaskCap = 0;
+            HIP_TRY(hipMalloc(&ms->tileMask, need * sizeof(unsigned long long)));
+            ms->tileMaskCap = need;
+        }
+    }
     if (s->triPadded > 0)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->primF,
                            s->primX, s->triPadded, P.origin);
+    if (cull) {
+        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, s->tileMask);
+        P.tileMask = s->tileMask;
+    }
     const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     if (P.sphereCount > 0 && debug)
         hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, st, P);
@@ -807,6 +937,8 @@ template <typename T> struct DevBuf {
     }
 };
 
+constexpr size_t kSegBytes = RTC_SEGMENT_COUNTERS * sizeof(unsigned long long);
+
 extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                           const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int device,
                           Color *outImage, float *outAccum, RtcStats *stats)
@@ -830,8 +962,8 @@ extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *sphe
     HIP_TRY(hipMalloc(&dColors.p, px * 3 + 16));
     if (outAccum)
         HIP_TRY(hipMalloc(&dAccum.p, px * 3 * sizeof(float) + 16));
-    HIP_TRY(hipMalloc(&dSeg.p, 2 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dSeg.p, 0, 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dSeg.p, kSegBytes));
+    HIP_TRY(hipMemset(dSeg.p, 0, kSegBytes));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -851,12 +983,13 @@ extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *sphe
     HIP_TRY(hipMemcpy(outImage, dColors.p, px * 3, hipMemcpyDeviceToHost));
     if (outAccum)
         HIP_TRY(hipMemcpy(outAccum, dAccum.p, px * 3 * sizeof(float), hipMemcpyDeviceToHost));
-    unsigned long long seg[2] = {0, 0};
-    HIP_TRY(hipMemcpy(seg, dSeg.p, sizeof seg, hipMemcpyDeviceToHost));
+    unsigned long long seg[RTC_SEGMENT_COUNTERS] = {0};
+    HIP_TRY(hipMemcpy(seg, dSeg.p, kSegBytes, hipMemcpyDeviceToHost));
     if (stats) {
         stats->renderMs = ms;
         stats->segments = seg[0];
         stats->samples = (unsigned long long)px * (unsigned long long)(d->spp > 0 ? d->spp : 0);
+        stats->triTests = seg[2];
         stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
@@ -920,9 +1053,9 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         if (e == hipSuccess && outAccum)
             e = hipMalloc(&p.acc, px * 3 * sizeof(float) + 16);
         if (e == hipSuccess)
-            e = hipMalloc(&p.seg, 2 * sizeof(unsigned long long));
+            e = hipMalloc(&p.seg, kSegBytes);
         if (e == hipSuccess)
-            e = hipMemsetAsync(p.seg, 0, 2 * sizeof(unsigned long long), p.st);
+            e = hipMemsetAsync(p.seg, 0, kSegBytes, p.st);
         if (e == hipSuccess)
             e = hipEventCreate(&p.e0);
         if (e == hipSuccess)
@@ -938,7 +1071,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             rc = rtc_fail(-(int)e, "event record: %s", hipGetErrorString(e));
     }
     double maxMs = 0;
-    unsigned long long segs = 0;
+    unsigned long long segs = 0, tests = 0;
     std::vector<unsigned char> col;
     std::vector<float> acc;
     for (int g = 0; g < numDevices && !rc; ++g) {
@@ -950,11 +1083,11 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             e = hipEventElapsedTime(&ms, p.e0, p.e1);
         const size_t px = (size_t)p.rows * (size_t)d->width;
         col.resize(px * 3 + 1);
-        unsigned long long sg[2] = {0, 0};
+        unsigned long long sg[RTC_SEGMENT_COUNTERS] = {0};
         if (e == hipSuccess)
             e = hipMemcpy(col.data(), p.col, px * 3, hipMemcpyDeviceToHost);
         if (e == hipSuccess)
-            e = hipMemcpy(sg, p.seg, sizeof sg, hipMemcpyDeviceToHost);
+            e = hipMemcpy(sg, p.seg, kSegBytes, hipMemcpyDeviceToHost);
         if (e == hipSuccess && outAccum) {
             acc.resize(px * 3 + 1);
             e = hipMemcpy(acc.data(), p.acc, px * 3 * sizeof(float), hipMemcpyDeviceToHost);
@@ -966,6 +1099,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         if (ms > maxMs)
             maxMs = ms;
         segs += sg[0];
+        tests += sg[2];
         const size_t rowB = (size_t)d->width * 3;
         for (int k = 0; k < p.rows; ++k) {
             const int y = g + k * numDevices;
@@ -981,6 +1115,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         stats->renderMs = maxMs;
         stats->segments = segs;
         stats->samples = (unsigned long long)d->width * d->height * (unsigned long long)(d->spp > 0 ? d->spp : 0);
+        stats->triTests = tests;
         stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;

@@ -118,6 +118,67 @@ def test_hoisted_primary_is_bit_exact(name, gpu_available):
     assert s0["segments"] == s1["segments"]
 
 
+@pytest.mark.parametrize("name", ["default_160x90x4", "ultracomplex_160x90x4", "fsuzane_odd_33x17x3",
+                                  "complex_64x36x16", "cube_64x36x4", "default_b1_32x18x4",
+                                  "ultracomplex_cam_96x64x8", "rsuzanne_160x90x4", "suze_quads_64x36x4"])
+@pytest.mark.parametrize("hoist", [False, True])
+def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
+    """Primary segments over the 8x8 tile's candidate list (rtc_tile_cull) == brute force over every
+    triangle (RTC_F_NO_TILE_CULL, what calculateRayCollision does): same bits, same paths, fewer tests."""
+    g = GOLD[name]
+    tris, tonly = load_tris(g["scene"])
+    sph = scene_spheres(g["scene"])
+    scene, cam, mb = setup_from_flags(g["flags"])
+    base = rt.RenderConfig(g["width"], g["height"], g["spp"], mb, bool(tonly), hoist)
+    c0, a0, s0 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "tile_cull": False}),
+                           want_accum=True)
+    c1, a1, s1 = rt.render(tris, sph, scene, cam, base, want_accum=True)
+    assert np.array_equal(_bits(a0), _bits(a1)) and np.array_equal(c0, c1)
+    assert s0["segments"] == s1["segments"]
+    assert s1["tri_tests"] <= s0["tri_tests"]
+    print(f"{name} hoist={hoist}: tests {s0['tri_tests']} -> {s1['tri_tests']}")
+
+
+def test_tile_cull_many_triangles(gpu_available):
+    """A synthetic 500-triangle scene (5 shifted copies of complex.obj; 8 mask words per tile): culled ==
+    brute force bit for bit, and both match the oracle."""
+    base_tris, tonly = load_tris("complex")
+    copies = []
+    for k, (dx, dz) in enumerate([(0, 0), (2.5, 0), (-2.5, 0), (0, 2.5), (0, -2.5)]):
+        t = base_tris.copy()
+        for v in ("posA", "posB", "posC"):
+            t[v]["x"] += np.float32(dx)
+            t[v]["z"] += np.float32(dz)
+        copies.append(t)
+    tris = np.concatenate(copies)
+    assert len(tris) == 500
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(96, 54, 4, 10, True)
+    c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**cfg.__dict__, "tile_cull": False}),
+                           want_accum=True)
+    c1, a1, s1 = rt.render(tris, None, scene, cam, cfg, want_accum=True)
+    assert np.array_equal(_bits(a0), _bits(a1)) and s0["segments"] == s1["segments"]
+    ocol, oacc, oseg = orc.render(tris, None, scene, cam, RtcRenderDesc(96, 54, 4, 10, tonly, 0, 1, 0), threads=8)
+    mx, over, _ = _compare(a1, oacc)
+    assert over == 0 and s1["segments"] == oseg
+
+
+def test_tile_cull_full_frame(gpu_available):
+    """The BASELINE frame (ultracomplex 1920x1080, 16 spp here): culled == brute force bit for bit, and the
+    culled run evaluates far fewer ray-triangle tests."""
+    tris, tonly = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(1920, 1080, 16, 10, True)
+    c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**cfg.__dict__, "tile_cull": False}),
+                           want_accum=True)
+    c1, a1, s1 = rt.render(tris, None, scene, cam, cfg, want_accum=True)
+    assert np.array_equal(_bits(a0), _bits(a1)) and s0["segments"] == s1["segments"]
+    assert s0["tri_tests"] == s0["segments"] * len(tris)
+    assert s1["tri_tests"] < s0["tri_tests"] // 4
+    print(f"1080p x16: brute {s0['render_ms']:.3f} ms, culled {s1['render_ms']:.3f} ms; "
+          f"tests {s0['tri_tests']} -> {s1['tri_tests']}")
+
+
 @pytest.mark.parametrize("scene,mb", [("default", 10), ("ultracomplex", 10), ("default", 3), ("fsuzane", 0)])
 def test_debug_bounce_integrator(scene, mb, gpu_available):
     """calcDebugColor (raytracing.c:242-260) as a kernel variant (RTC_F_DEBUG_BOUNCES) == the oracle's, which

@@ -35,6 +35,7 @@ QUICK = "--quick" in sys.argv
 if not DIAG:
     variants = {
         "faithful": (tris, rt.RenderConfig(W, H, SPP, 10, True)),
+        "faithful_nocull": (tris, rt.RenderConfig(W, H, SPP, 10, True, tile_cull=False)),
         "hoist": (tris, rt.RenderConfig(W, H, SPP, 10, True, hoist=True)),
         "mb1": (tris, rt.RenderConfig(W, H, SPP, 1, True)),
         "mb1_hoist": (tris, rt.RenderConfig(W, H, SPP, 1, True, hoist=True)),
@@ -44,10 +45,10 @@ if not DIAG:
         "spp16": (tris, rt.RenderConfig(W, H, 16, 10, True)),
     }
     if QUICK:
-        variants = {k: variants[k] for k in ("faithful", "hoist", "mb1", "empty_scene")}
+        variants = {k: variants[k] for k in ("faithful", "faithful_nocull", "hoist", "mb1", "empty_scene")}
     for k, (t, cfg) in variants.items():
         st = timed(t, cfg)
-        print(json.dumps({"variant": k, "T": len(t), "ms": round(st["render_ms"], 3), "segments": st["segments"],
+        print(json.dumps({"variant": k, "T": len(t), "ms": round(st["render_ms"], 3), "segments": st["segments"], "tri_tests": st["tri_tests"],
                           "mrays": round(st["samples"] / st["render_ms"] / 1e3, 1)}), flush=True)
 else:
     for hoist in (False, True):

@@ -12,7 +12,8 @@ from conftest import load_tris  # noqa: E402
 v = sys.argv[1] if len(sys.argv) > 1 else "faithful"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 tris, _ = load_tris("ultracomplex")
-cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
+cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True),
+       "nocull": rt.RenderConfig(1920, 1080, 64, 10, True, tile_cull=False), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
        "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
        "empty": rt.RenderConfig(1920, 1080, 64, 10, True)}[v]
 if v == "empty":
