@@ -57,6 +57,8 @@ typedef struct RtcRenderDesc {
 #define RTC_F_DEBUG_BOUNCES 0x2  /* calcDebugColor (raytracing.c:242-260) instead of calcColor: bounce-count grey */
 #define RTC_F_NO_TILE_CULL  0x4  /* primary segments test every triangle (brute force, as calculateRayCollision
                                     does) instead of the 8x8 tile's candidate list; same output bit for bit */
+#define RTC_F_NO_REORDER    0x8  /* dispatch workgroups in raster order instead of heaviest first (for A/B
+                                    timing; the frame is identical) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */

@@ -136,10 +136,11 @@ struct RtcDeviceScene {
     DevSphere *spheres;
     DevPrimF *primF; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
     DevPrimX *primX;
-    /* per-launch scratch, written by rtc_tile_cull: one candidate bit-set of maskWords u64 per 8x8 tile */
-    unsigned long long *tileMask;
-    size_t tileMaskCap; /* capacity, u64 words */
-    int maskWords;      /* ceil(triPadded / 64) */
+    /* per-launch scratch (rtc_tile_cull / rtc_order_blocks): the candidate bit-sets (maskWords u64 per 8x8
+     * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
+    unsigned char *scratch;
+    size_t scratchCap; /* bytes */
+    int maskWords;     /* ceil(triPadded / 64) */
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -255,8 +256,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->primF);
     if (s->primX)
         (void)hipFree(s->primX);
-    if (s->tileMask)
-        (void)hipFree(s->tileMask);
+    if (s->scratch)
+        (void)hipFree(s->scratch);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -278,6 +279,7 @@ struct RenderParams {
     const DevPrimF *__restrict__ primF;
     const DevPrimX *__restrict__ primX;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
+    const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
@@ -301,13 +303,13 @@ struct PixelRay {
     V3 dir;
 };
 
-__device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P)
+__device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P, int bx, int by)
 {
     PixelRay px;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    px.x = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
-    px.r = blockIdx.y * kTileH + (wave >> 1) * 8 + (lane >> 3);
+    px.x = bx * kTileW + (wave & 1) * 8 + (lane & 7);
+    px.r = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
     px.valid = px.x < P.width && px.r < P.rows;
     px.y = P.rowStart + px.r * P.rowStride;
     /* integer halves, then int->float, f32 divide */
@@ -318,10 +320,25 @@ __device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P)
 }
 
 /* This wave's 8x8 tile in the launch (made provably wave-uniform, so tile data is scalar-loaded). */
-__device__ __forceinline__ int wave_tile()
+__device__ __forceinline__ int wave_tile(int bx, int by)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return (blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1);
+    return (by * 2 + (wave >> 1)) * (gridDim.x * 2) + bx * 2 + (wave & 1);
+}
+
+/* The workgroup this launch slot renders.  Workgroups are dispatched in launch-slot order; with P.order
+ * (rtc_order_blocks) the ones whose pixels see geometry -- the long-running ones -- go first, so the many
+ * short sky-only workgroups fill in behind them instead of leaving them as a tail. */
+__device__ __forceinline__ void block_xy(const RenderParams &P, int &bx, int &by)
+{
+    if (P.order) {
+        const int id = P.order[blockIdx.y * gridDim.x + blockIdx.x];
+        bx = id % (int)gridDim.x;
+        by = id / (int)gridDim.x;
+    } else {
+        bx = blockIdx.x;
+        by = blockIdx.y;
+    }
 }
 
 /* Error bounds for the primary filter (u = 2^-24, |d_i| <= 1 + 2^-22 for a normalized float direction).
@@ -602,23 +619,71 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
  * of the tile, so the reference's rayTriangle rejects it for every primary ray there: the closest hit is
  * unchanged, bit for bit.  The filter is the render kernel's own (prim_backfacing / prim_pass, same records,
  * same pixel_ray). */
-__global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask)
+__global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
+                                                       unsigned *__restrict__ weight)
 {
-    const PixelRay px = pixel_ray(P);
+    __shared__ unsigned wgWeight;
+    if (threadIdx.x == 0)
+        wgWeight = 0;
+    __syncthreads();
+    const int bx = blockIdx.x, by = blockIdx.y;
+    const PixelRay px = pixel_ray(P, bx, by);
     const int lane = threadIdx.x & 63;
-    unsigned long long *out = mask + (size_t)wave_tile() * P.maskWords;
+    unsigned long long *out = mask + (size_t)wave_tile(bx, by) * P.maskWords;
+    bool anyCand = false;
     for (int w = 0; w < P.maskWords; ++w) {
         unsigned long long bits = 0;
-        const int n = min(64, P.triPadded - w * 64);
-        for (int k = 0; k < n; ++k) {
-            const DevPrimF F = P.primF[w * 64 + k];
-            const bool keep = px.valid && !prim_backfacing(px.dir, F) && prim_pass(px.dir, F);
-            if (__any(keep))
-                bits |= 1ull << k;
+        const int n = min(64, P.triPadded - w * 64); /* a multiple of 8 */
+        for (int k0 = 0; k0 < n; k0 += 4) {
+            DevPrimF F[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                F[j] = P.primF[w * 64 + k0 + j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool keep = (int)px.valid & (int)!prim_backfacing(px.dir, F[j]) & (int)prim_pass(px.dir, F[j]);
+                anyCand |= keep;
+                if (__ballot(keep))
+                    bits |= 1ull << (k0 + j);
+            }
         }
         if (lane == 0)
             out[w] = bits;
     }
+    /* workgroup weight: pixels with at least one candidate (they do the bounce work) */
+    const unsigned long long b = __ballot(anyCand);
+    if (lane == 0 && b)
+        atomicAdd(&wgWeight, (unsigned)__popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0)
+        weight[blockIdx.y * gridDim.x + blockIdx.x] = wgWeight;
+}
+
+/* Launch order of the render kernel's workgroups: a counting sort of the weights, heaviest bucket first
+ * (order inside a bucket is arbitrary; the frame does not depend on it -- every pixel is seeded by its own
+ * index, main.c:95).  One workgroup; n is at most a few ten thousand. */
+constexpr int kOrderBuckets = 17; /* weight / 16: 0 (sky only) .. 16 (all 256 pixels see geometry) */
+__global__ __launch_bounds__(1024) void rtc_order_blocks(const unsigned *__restrict__ weight, int n,
+                                                          int *__restrict__ order)
+{
+    __shared__ int cnt[kOrderBuckets];
+    if (threadIdx.x < kOrderBuckets)
+        cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        atomicAdd(&cnt[min(kOrderBuckets - 1, (int)((weight[i] + 15) / 16))], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int b = kOrderBuckets - 1; b >= 0; --b) {
+            const int c = cnt[b];
+            cnt[b] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        order[atomicAdd(&cnt[min(kOrderBuckets - 1, (int)((weight[i] + 15) / 16))], 1)] = i;
 }
 
 #ifdef RTC_DIAG
@@ -643,7 +708,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     unsigned diagIters = 0;
 #endif
     const int lane = threadIdx.x & 63;
-    const PixelRay px = pixel_ray(P);
+    int bx, by;
+    block_xy(P, bx, by);
+    const PixelRay px = pixel_ray(P, bx, by);
     const int x = px.x, r = px.r, y = px.y;
     const bool valid = px.valid;
     const V3 pdir = px.dir;
@@ -653,7 +720,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     const unsigned long long *tmask = nullptr;
     unsigned listLen = (unsigned)P.triCount;
     if (P.tileMask) {
-        tmask = P.tileMask + (size_t)wave_tile() * P.maskWords;
+        tmask = P.tileMask + (size_t)wave_tile(bx, by) * P.maskWords;
         listLen = 0;
         for (int w = 0; w < P.maskWords; ++w)
             listLen += (unsigned)__popcll(tmask[w]);
@@ -863,27 +930,35 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     hipStream_t st = (hipStream_t)stream;
     P.primF = s->primF;
     P.primX = s->primX;
-    /* tile candidate lists: one bit-set per 8x8 tile (4 per workgroup), grown on demand (hipFree
-     * synchronises, so a previous launch still reading the old buffer has finished) */
+    /* tile candidate lists (one bit-set per 8x8 tile, 4 per workgroup), workgroup weights and the dispatch
+     * order, in one scratch buffer grown on demand (hipFree synchronises, so a previous launch still reading
+     * the old buffer has finished) */
     const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords > 0;
+    const size_t blocks = (size_t)grid.x * grid.y;
+    const size_t maskBytes = blocks * 4 * (size_t)s->maskWords * sizeof(unsigned long long);
     if (cull) {
-        const size_t need = (size_t)grid.x * 2 * grid.y * 2 * (size_t)s->maskWords;
-        if (need > s->tileMaskCap) {
+        const size_t need = maskBytes + 2 * blocks * sizeof(int);
+        if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
-            if (ms->tileMask)
-                HIP_TRY(hipFree(ms->tileMask));
-            ms->tileMask = nullptr;
-            ms->tileMaskCap = 0;
-            HIP_TRY(hipMalloc(&ms->tileMask, need * sizeof(unsigned long long)));
-            ms->tileMaskCap = need;
+            if (ms->scratch)
+                HIP_TRY(hipFree(ms->scratch));
+            ms->scratch = nullptr;
+            ms->scratchCap = 0;
+            HIP_TRY(hipMalloc(&ms->scratch, need));
+            ms->scratchCap = need;
         }
     }
     if (s->triPadded > 0)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->primF,
                            s->primX, s->triPadded, P.origin);
     if (cull) {
-        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, s->tileMask);
-        P.tileMask = s->tileMask;
+        unsigned long long *mask = (unsigned long long *)s->scratch;
+        unsigned *weight = (unsigned *)(s->scratch + maskBytes);
+        int *order = (int *)(s->scratch + maskBytes + blocks * sizeof(int));
+        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight);
+        hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
+        P.tileMask = mask;
+        P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
     }
     const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     if (P.sphereCount > 0 && debug)

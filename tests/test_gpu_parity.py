@@ -175,7 +175,11 @@ def test_tile_cull_full_frame(gpu_available):
     assert np.array_equal(_bits(a0), _bits(a1)) and s0["segments"] == s1["segments"]
     assert s0["tri_tests"] == s0["segments"] * len(tris)
     assert s1["tri_tests"] < s0["tri_tests"] // 4
-    print(f"1080p x16: brute {s0['render_ms']:.3f} ms, culled {s1['render_ms']:.3f} ms; "
+    c2, a2, s2 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**cfg.__dict__, "reorder": False}),
+                           want_accum=True)
+    assert np.array_equal(_bits(a1), _bits(a2)) and s1["segments"] == s2["segments"]
+    print(f"1080p x16: brute {s0['render_ms']:.3f} ms, culled {s1['render_ms']:.3f} ms, raster order "
+          f"{s2['render_ms']:.3f} ms; "
           f"tests {s0['tri_tests']} -> {s1['tri_tests']}")
 
 

@@ -36,6 +36,7 @@ if not DIAG:
     variants = {
         "faithful": (tris, rt.RenderConfig(W, H, SPP, 10, True)),
         "faithful_nocull": (tris, rt.RenderConfig(W, H, SPP, 10, True, tile_cull=False)),
+        "faithful_raster": (tris, rt.RenderConfig(W, H, SPP, 10, True, reorder=False)),
         "hoist": (tris, rt.RenderConfig(W, H, SPP, 10, True, hoist=True)),
         "mb1": (tris, rt.RenderConfig(W, H, SPP, 1, True)),
         "mb1_hoist": (tris, rt.RenderConfig(W, H, SPP, 1, True, hoist=True)),
@@ -45,14 +46,14 @@ if not DIAG:
         "spp16": (tris, rt.RenderConfig(W, H, 16, 10, True)),
     }
     if QUICK:
-        variants = {k: variants[k] for k in ("faithful", "faithful_nocull", "hoist", "mb1", "empty_scene")}
+        variants = {k: variants[k] for k in ("faithful", "faithful_nocull", "faithful_raster", "hoist", "mb1", "empty_scene")}
     for k, (t, cfg) in variants.items():
         st = timed(t, cfg)
         print(json.dumps({"variant": k, "T": len(t), "ms": round(st["render_ms"], 3), "segments": st["segments"], "tri_tests": st["tri_tests"],
                           "mrays": round(st["samples"] / st["render_ms"] / 1e3, 1)}), flush=True)
 else:
-    for hoist in (False, True):
-        cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist)
+    for hoist, reorder in ((False, True), (False, False), (True, True)):
+        cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, reorder=reorder)
         nw = ((W + 15) // 16) * ((H + 15) // 16) * 4
         buf = torch.zeros(nw * 3, dtype=torch.int64, device="cuda")
         rt.lib().rtc_diag_set_buffer.argtypes = [C.c_void_p]
@@ -63,7 +64,7 @@ else:
         cyc, it, t0 = d[:, 0].astype(np.float64), d[:, 1], d[:, 2]
         span = (t0 + d[:, 0]).max() - t0.min()
         q = lambda a, p: float(np.percentile(a, p))
-        print(json.dumps({"hoist": hoist, "kernel_ms": round(st["render_ms"], 3), "waves": nw,
+        print(json.dumps({"hoist": hoist, "reorder": reorder, "kernel_ms": round(st["render_ms"], 3), "waves": nw,
                           "cycles_p50": q(cyc, 50), "cycles_p90": q(cyc, 90), "cycles_p99": q(cyc, 99),
                           "cycles_max": float(cyc.max()), "cycles_sum": float(cyc.sum()),
                           "iters_p50": q(it, 50), "iters_p99": q(it, 99), "iters_max": int(it.max()),
@@ -71,4 +72,4 @@ else:
                           "share_waves_over_2x_median": float((cyc > 2 * np.median(cyc)).mean()),
                           "cycles_in_waves_over_2x_median": float(cyc[cyc > 2 * np.median(cyc)].sum() / cyc.sum()),
                           }), flush=True)
-        np.save(os.path.join(REPO, "gpurun_out", f"wavecycles_hoist{int(hoist)}.npy"), d)
+        np.save(os.path.join(REPO, "gpurun_out", f"wavecycles_hoist{int(hoist)}_reorder{int(reorder)}.npy"), d)
