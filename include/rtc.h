@@ -59,6 +59,8 @@ typedef struct RtcRenderDesc {
                                     does) instead of the 8x8 tile's candidate list; same output bit for bit */
 #define RTC_F_NO_REORDER    0x8  /* dispatch workgroups in raster order instead of heaviest first (for A/B
                                     timing; the frame is identical) */
+#define RTC_F_NO_COOP       0x10 /* tiles that see geometry keep one lane per pixel instead of a workgroup
+                                    with 4 cooperating lanes per pixel (A/B timing; the frame is identical) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */

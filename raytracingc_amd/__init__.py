@@ -26,6 +26,7 @@ from ._abi import (  # noqa: F401
     RAY_DT,
     RTC_F_DEBUG_BOUNCES,
     RTC_F_HOIST_PRIMARY,
+    RTC_F_NO_COOP,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
     RTC_SEGMENT_COUNTERS,
@@ -130,10 +131,12 @@ class RenderConfig:
     debug_bounces: bool = False  # calcDebugColor (raytracing.c:242-260) instead of calcColor
     tile_cull: bool = True  # primary segments visit their 8x8 tile's candidate triangles (bit-exact)
     reorder: bool = True  # dispatch the workgroups that see geometry first (same frame)
+    coop: bool = True  # tiles that see geometry: 4 cooperating lanes per pixel (same frame)
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
-                | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER))
+                | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
+                | (0 if self.coop else RTC_F_NO_COOP))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),

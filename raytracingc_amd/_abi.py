@@ -78,6 +78,7 @@ RTC_F_HOIST_PRIMARY = 0x1
 RTC_F_DEBUG_BOUNCES = 0x2
 RTC_F_NO_TILE_CULL = 0x4
 RTC_F_NO_REORDER = 0x8
+RTC_F_NO_COOP = 0x10
 RTC_SEGMENT_COUNTERS = 4  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 

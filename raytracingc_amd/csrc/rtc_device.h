@@ -51,7 +51,12 @@ __device__ __forceinline__ float random_value(unsigned &s)
     s = s * 747796405u + 2891336453u;
     unsigned r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;
     r = (r >> 22) ^ r;
-    return (float)((double)r / 4294967295.0);
+    /* (float)((double)r / 4294967295.0) without the double divide: r/(2^32-1) = r 2^-32 (1 + 2^-32 + ...)
+     * lies within r 2^-64 (< 2^-32) above r 2^-32, which cannot reach the next float rounding boundary but
+     * does push an exact tie upward; r 2^-32 + r 2^-64 (one rounding) does the same.  Equal for all 2^32
+     * values of r (checked exhaustively, tools/check_devmath.cpp). */
+    const double d = (double)r * 0x1p-32;
+    return (float)fma((double)r, 0x1p-64, d);
 }
 /* RandomValueNormalDistrubtion (moremath.c:97-102): Box-Muller cos branch in double */
 __device__ __forceinline__ float random_normal(unsigned &s)
@@ -69,10 +74,10 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
     return normalized(V3{a, b, c});
 }
 
-/* powf for the environment (raytracing.c:153,155): evaluated in double and rounded once (rtc_math.h).
- * glibc's powf is within 0.82 ulp, so the two differ by 1 ulp on a small fraction of arguments (covered
- * by the float tolerance; tools/check_devmath.cpp counts them). */
-__device__ __forceinline__ float pow_ref(float x, float y) { return rtcmath::pow_ref(x, y); }
+/* powf for the environment (raytracing.c:153,155): glibc 2.35's own powf algorithm, tables and
+ * coefficients, as its x86-64 FMA build evaluates it (rtc_math.h powf_glibc): bit-identical to the
+ * reference's powf calls (tools/check_devmath.cpp: every float x in [0, 1] for the exponents checked). */
+__device__ __forceinline__ float pow_ref(float x, float y) { return rtcmath::powf_glibc<true>(x, y); }
 
 struct EnvParams {
     V3 sun, horizon, zenith, ground;

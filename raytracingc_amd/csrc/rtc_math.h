@@ -189,6 +189,197 @@ RTC_HD double exp2(double t)
     return ldexp(p, (int)k);
 }
 
+/* ---- glibc's powf, restated -----------------------------------------------------------------------------
+ * The reference calls powf (raytracing.c:153,155) from glibc 2.35 libm.  That powf is ARM's optimized-routines
+ * algorithm (sysdeps/ieee754/flt-32/e_powf.c, published under MIT / Apache-2.0): log2(x) from a 16-entry
+ * {1/c, log2 c} table and a degree-5 polynomial in r = z/c - 1, then y*log2(x), then 2^t from a 32-entry table
+ * of 2^(i/32) and a degree-3 polynomial, all in double, with ONE final rounding to float.  It is not correctly
+ * rounded (<= 0.82 ulp), so matching it bit for bit needs the same tables, coefficients and operation order.
+ * On x86-64 glibc picks its FMA build (__powf_fma) on every CPU with FMA + AVX2; that build contracts each
+ * a*b+c below into a fused multiply-add (FMA = true).  The table and coefficient values are glibc's
+ * __powf_log2_data / __exp2f_data (tools/extract_glibc_powf.py reads them out of libm.so.6);
+ * tools/check_devmath.cpp checks this restatement against libm's powf on every float x in [0, 1]. */
+namespace powf_data {
+constexpr double kLog2Tab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2}, {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2},
+    {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2}, {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2},
+    {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2}, {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3}, {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4},
+    {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4},  {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3},
+    {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
+    {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2},  {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2},
+};
+constexpr double kLog2Poly[5] = {0x1.27616c9496e0bp-2, -0x1.71969a075c67ap-2, 0x1.ec70a6ca7baddp-2,
+                                 -0x1.7154748bef6c8p-1, 0x1.71547652ab82bp+0};
+/* asuint64(2^(i/32)) - (i << 47) */
+constexpr unsigned long long kExp2Tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull,
+};
+constexpr double kExp2Poly[3] = {0x1.c6af84b912394p-5, 0x1.ebfce50fac4f3p-3, 0x1.62e42ff0c52d6p-1};
+constexpr double kExp2Shift = 0x1.8p+52 / 32; /* __exp2f_data.shift_scaled */
+constexpr unsigned kSignBias = 1u << (5 + 11);
+} // namespace powf_data
+
+RTC_HD unsigned f2u(float f)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __float_as_uint(f);
+#else
+    unsigned u;
+    memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+RTC_HD float u2f(unsigned u)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __uint_as_float(u);
+#else
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+#endif
+}
+RTC_HD unsigned long long d2u(double d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (unsigned long long)__double_as_longlong(d);
+#else
+    unsigned long long u;
+    memcpy(&u, &d, 8);
+    return u;
+#endif
+}
+RTC_HD double u2d(unsigned long long u)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double((long long)u);
+#else
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+#endif
+}
+
+/* a*b + c as the chosen glibc build evaluates it: fused (FMA build) or two roundings */
+template <bool FMA> RTC_HD double mad(double a, double b, double c) { return FMA ? fma(a, b, c) : a * b + c; }
+
+/* 0: not an integer, 1: odd integer, 2: even integer (e_powf.c checkint) */
+RTC_HD int powf_checkint(unsigned iy)
+{
+    const int e = (int)(iy >> 23 & 0xff);
+    if (e < 0x7f)
+        return 0;
+    if (e > 0x7f + 23)
+        return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1))
+        return 0;
+    if (iy & (1u << (0x7f + 23 - e)))
+        return 1;
+    return 2;
+}
+RTC_HD bool powf_zeroinfnan(unsigned ix) { return 2 * ix - 1 >= 2u * 0x7f800000u - 1; }
+
+template <bool FMA> RTC_HD double powf_log2(unsigned ix) /* e_powf.c log2_inline */
+{
+    const unsigned tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> (23 - 4)) % 16);
+    const unsigned top = tmp & 0xff800000u;
+    const unsigned iz = ix - top;
+    const int k = (int)top >> 23; /* arithmetic shift */
+    const double invc = powf_data::kLog2Tab[i][0], logc = powf_data::kLog2Tab[i][1];
+    const double z = (double)u2f(iz);
+    const double r = mad<FMA>(z, invc, -1.0);
+    const double y0 = logc + (double)k;
+    const double *A = powf_data::kLog2Poly;
+    const double r2 = r * r;
+    double y = mad<FMA>(A[0], r, A[1]);
+    const double p = mad<FMA>(A[2], r, A[3]);
+    const double r4 = r2 * r2;
+    double q = mad<FMA>(A[4], r, y0);
+    q = mad<FMA>(p, r2, q);
+    y = mad<FMA>(y, r4, q);
+    return y;
+}
+
+template <bool FMA> RTC_HD float powf_exp2(double xd, unsigned signBias) /* e_powf.c exp2_inline */
+{
+    double kd = xd + powf_data::kExp2Shift;
+    const unsigned long long ki = d2u(kd);
+    kd -= powf_data::kExp2Shift;
+    const double r = xd - kd;
+    unsigned long long t = powf_data::kExp2Tab[ki % 32];
+    const unsigned long long ski = ki + signBias;
+    t += ski << (52 - 5);
+    const double s = u2d(t);
+    const double *C = powf_data::kExp2Poly;
+    const double z = mad<FMA>(C[0], r, C[1]);
+    const double r2 = r * r;
+    double y = mad<FMA>(C[2], r, 1.0);
+    y = mad<FMA>(z, r2, y);
+    y = y * s;
+    return (float)y;
+}
+
+template <bool FMA> RTC_HD float powf_glibc(float x, float y) /* e_powf.c __powf, round-to-nearest */
+{
+    unsigned signBias = 0;
+    unsigned ix = f2u(x), iy = f2u(y);
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || powf_zeroinfnan(iy)) {
+        if (powf_zeroinfnan(iy)) {
+            /* signalling NaN: quiet bit clear */
+            auto sig = [](unsigned u) { return (u & 0x7fc00000u) == 0x7f800000u && (u & 0x003fffffu) != 0; };
+            if (2 * iy == 0)
+                return sig(ix) ? x + y : 1.0f;
+            if (ix == 0x3f800000u)
+                return sig(iy) ? x + y : 1.0f;
+            if (2 * ix > 2u * 0x7f800000u || 2 * iy > 2u * 0x7f800000u)
+                return x + y;
+            if (2 * ix == 2u * 0x3f800000u)
+                return 1.0f;
+            if ((2 * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u))
+                return 0.0f;
+            return y * y;
+        }
+        if (powf_zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && powf_checkint(iy) == 1)
+                x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        if (ix & 0x80000000u) { /* finite x < 0 */
+            const int yint = powf_checkint(iy);
+            if (yint == 0)
+                return __builtin_nanf("");
+            if (yint == 1)
+                signBias = powf_data::kSignBias;
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) { /* subnormal x: normalise */
+            ix = f2u(x * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
+    }
+    const double logx = powf_log2<FMA>(ix);
+    const double ylogx = (double)y * logx;
+    if ((d2u(ylogx) >> 47 & 0xffff) >= d2u(126.0) >> 47) {
+        if (ylogx > 0x1.fffffffd1d571p+6)
+            return signBias ? -__builtin_inff() : __builtin_inff();
+        if (ylogx <= -150.0)
+            return signBias ? -0.0f : 0.0f;
+    }
+    return powf_exp2<FMA>(ylogx, signBias);
+}
+
 /* powf(x, y) of raytracing.c:153,155 for x >= 0 (or NaN): exp2(y * log2(x)) in double, rounded once */
 RTC_HD float pow_ref(float x, float y)
 {

@@ -280,6 +280,7 @@ struct RenderParams {
     const DevPrimX *__restrict__ primX;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
+    int blocksX; /* 16x16 blocks per row of the launch */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
@@ -303,6 +304,14 @@ struct PixelRay {
     V3 dir;
 };
 
+__device__ __forceinline__ V3 primary_dir(const RenderParams &P, int x, int y)
+{
+    /* integer halves, then int->float, f32 divide */
+    const float dx = (float)(x - P.width / 2) / (float)(P.height / 2);
+    const float dy = (float)(y - P.height / 2) / (float)(P.height / 2);
+    return normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
+}
+
 __device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P, int bx, int by)
 {
     PixelRay px;
@@ -312,10 +321,7 @@ __device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P, int bx, int
     px.r = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
     px.valid = px.x < P.width && px.r < P.rows;
     px.y = P.rowStart + px.r * P.rowStride;
-    /* integer halves, then int->float, f32 divide */
-    const float dx = (float)(px.x - P.width / 2) / (float)(P.height / 2);
-    const float dy = (float)(px.y - P.height / 2) / (float)(P.height / 2);
-    px.dir = normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
+    px.dir = primary_dir(P, px.x, px.y);
     return px;
 }
 
@@ -542,41 +548,89 @@ __device__ __forceinline__ void closest_primary_listed(const RenderParams &P, V3
 }
 
 /* General segments (any origin): rayTriangle (raytracing.c:186-214) with AB, AC precomputed. */
+__device__ __forceinline__ void general_test(V3 pos, V3 dir, const DevTri &R, int idx, Closest &c)
+{
+    const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
+    if (!(nd >= 0.f)) {
+        const V3 AB{R.abx, R.aby, R.abz}, AC{R.acx, R.acy, R.acz};
+        const V3 h = cross(dir, AC);
+        const float det = dot(AB, h);
+        const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
+        const float uu = dot(s, h);
+        const float r = __builtin_amdgcn_rcpf(det);
+        const float ua = uu * r;
+        const bool detOk = !(-kEps < det && det < kEps);
+        if (detOk & !(ua < -kTiny) & !(ua > 1.000001f)) {
+            const float invDet = 1.f / det;
+            const float u = uu * invDet;
+            const V3 q = cross(s, AB);
+            const float v = dot(dir, q) * invDet;
+            const float dst = dot(AC, q) * invDet;
+            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                c.dst = dst;
+                c.idx = idx;
+            }
+        }
+    }
+}
+
+/* Scenes up to kLdsTris triangles keep their general-path records in LDS (one copy per workgroup, loaded at
+ * kernel start): the general loop then reads them as broadcast ds_read_b128 instead of scalar loads that
+ * compete for the scalar cache with the primary records. */
+#ifndef RTC_GEN_LDS
+#define RTC_GEN_LDS 1
+#endif
+constexpr int kLdsTris = 256;
+
+__device__ __forceinline__ void closest_general_lds(const DevTri *__restrict__ lds, int Tp, V3 pos, V3 dir,
+                                                    Closest &c, int base)
+{
+    for (int t0 = 0; t0 < Tp; t0 += 2) {
+        const DevTri R0 = lds[t0], R1 = lds[t0 + 1];
+        general_test(pos, dir, R0, base + t0, c);
+        general_test(pos, dir, R1, base + t0 + 1, c);
+    }
+}
+
+#ifndef RTC_GEN_PF
+#define RTC_GEN_PF 1
+#endif
 __device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V3 dir, Closest &c, int base)
 {
     const int Tp = P.triPadded;
+#if RTC_GEN_PF
+    /* two alternating scalar-load batches, as closest_primary: the next records are in flight while the
+     * current ones are tested (the arrays carry 8 spare records) */
+    const DevTri *rec = P.tris;
+    DevTri A[kUnroll], B[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k)
+        A[k] = rec[k];
+    for (int t0 = 0; t0 < Tp; t0 += 2 * kUnroll, rec += 2 * kUnroll) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            B[k] = rec[kUnroll + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            general_test(pos, dir, A[k], base + t0 + k, c);
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            A[k] = rec[2 * kUnroll + k];
+#pragma unroll
+        for (int k = 0; k < kUnroll; ++k)
+            general_test(pos, dir, B[k], base + t0 + kUnroll + k, c);
+    }
+#else
     for (int t0 = 0; t0 < Tp; t0 += kUnroll) {
         DevTri RR[kUnroll];
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
             RR[k] = P.tris[t0 + k];
 #pragma unroll
-        for (int k = 0; k < kUnroll; ++k) {
-            const DevTri &R = RR[k];
-            const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
-            if (!(nd >= 0.f)) {
-                const V3 AB{R.abx, R.aby, R.abz}, AC{R.acx, R.acy, R.acz};
-                const V3 h = cross(dir, AC);
-                const float det = dot(AB, h);
-                const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
-                const float uu = dot(s, h);
-                const float r = __builtin_amdgcn_rcpf(det);
-                const float ua = uu * r;
-                const bool detOk = !(-kEps < det && det < kEps);
-                if (detOk & !(ua < -kTiny) & !(ua > 1.000001f)) {
-                    const float invDet = 1.f / det;
-                    const float u = uu * invDet;
-                    const V3 q = cross(s, AB);
-                    const float v = dot(dir, q) * invDet;
-                    const float dst = dot(AC, q) * invDet;
-                    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
-                        c.dst = dst;
-                        c.idx = base + t0 + k;
-                    }
-                }
-            }
-        }
+        for (int k = 0; k < kUnroll; ++k)
+            general_test(pos, dir, RR[k], base + t0 + k, c);
     }
+#endif
 }
 
 /* calculateRayCollision (raytracing.c:216-240): spheres first (only if !trianglesOnly), then triangles
@@ -586,7 +640,7 @@ __device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V
  * `mask` (wave-uniform, nullable) = the tile's primary candidates. */
 template <bool SPHERES>
 __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3 dir, bool primaryWave,
-                                               const unsigned long long *mask)
+                                               const unsigned long long *mask, const DevTri *lds)
 {
     Closest c{999999.f, -1};
     if (SPHERES) {
@@ -605,6 +659,8 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
             closest_primary_listed(P, dir, c, base, mask);
         else
             closest_primary(P, dir, c, base);
+    } else if (lds) {
+        closest_general_lds(lds, P.triPadded, pos, dir, c, base);
     } else {
         closest_general(P, pos, dir, c, base);
     }
@@ -620,7 +676,7 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
  * unchanged, bit for bit.  The filter is the render kernel's own (prim_backfacing / prim_pass, same records,
  * same pixel_ray). */
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
-                                                       unsigned *__restrict__ weight)
+                                                       unsigned *__restrict__ weight, unsigned *__restrict__ tileW)
 {
     __shared__ unsigned wgWeight;
     if (threadIdx.x == 0)
@@ -650,8 +706,11 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         if (lane == 0)
             out[w] = bits;
     }
-    /* workgroup weight: pixels with at least one candidate (they do the bounce work) */
+    /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
+     * non-empty candidate list exactly when its weight is > 0 */
     const unsigned long long b = __ballot(anyCand);
+    if (lane == 0)
+        tileW[wave_tile(bx, by)] = (unsigned)__popcll(b);
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
     __syncthreads();
@@ -687,7 +746,8 @@ __global__ __launch_bounds__(1024) void rtc_order_blocks(const unsigned *__restr
 }
 
 #ifdef RTC_DIAG
-/* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp} */
+/* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp, cycles inside
+ * closest_hit} */
 __device__ unsigned long long *g_rtc_diag = nullptr;
 extern "C" int rtc_diag_set_buffer(void *dptr)
 {
@@ -706,6 +766,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
 #ifdef RTC_DIAG
     const unsigned long long diagT0 = __builtin_amdgcn_s_memtime();
     unsigned diagIters = 0;
+    unsigned long long diagTrace = 0;
 #endif
     const int lane = threadIdx.x & 63;
     int bx, by;
@@ -715,6 +776,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     const bool valid = px.valid;
     const V3 pdir = px.dir;
     unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
+
+    /* general-path records in LDS (small scenes) */
+    __shared__ DevTri sTris[kLdsTris];
+    const bool useLds = RTC_GEN_LDS && P.triPadded <= kLdsTris;
+    if (useLds) {
+        for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
+            sTris[i] = P.tris[i];
+        __syncthreads();
+    }
+    const DevTri *lds = useLds ? sTris : nullptr;
 
     /* this wave's primary candidates (rtc_tile_cull) */
     const unsigned long long *tmask = nullptr;
@@ -740,11 +811,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     unsigned segCalls = 0, segTraced = 0;
     unsigned long long segTests = 0;
 
+    /* Sky tile (wave-uniform): no triangle is a primary candidate anywhere in this 8x8 tile and there are
+     * no spheres, so calculateRayCollision over the tile's (empty) candidate list misses for every primary
+     * ray here, and every sample of calcColor is that one miss: light = 0 + env(dir) * (1,1,1)
+     * (raytracing.c:268-293), acc += light * (float)(1/spp) (main.c:99).  Same operations as the state
+     * machine below, without its per-segment bookkeeping; the sample loop is unrolled for ILP. */
+    const bool skyTile = !DEBUG && !SPHERES && P.tileMask && listLen == 0;
+    if (skyTile) {
+        if (alive) {
+#pragma unroll 2
+            for (int s = 0; s < P.spp; ++s) {
+                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(pdir, P.env), V3{1.f, 1.f, 1.f}));
+                acc = add(acc, mul(l, P.invSpp));
+            }
+            segCalls = (unsigned)P.spp;
+            segTraced = P.hoist ? 1u : (unsigned)P.spp;
+        }
+        alive = false;
+    }
+
     /* bit-exact primary-hit hoisting: the primary ray consumes no RNG, so its closest hit
      * is a function of the pixel; trace it once instead of once per sample. */
     Closest primary{999999.f, -1};
     if (P.hoist && alive) {
-        primary = closest_hit<SPHERES>(P, pos, dir, true, tmask);
+        primary = closest_hit<SPHERES>(P, pos, dir, true, tmask, lds);
         segTraced++;
         segTests += listLen;
     }
@@ -762,7 +852,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
             if (!needTrace) {
                 c = primary;
             } else {
-                c = closest_hit<SPHERES>(P, pos, dir, primaryWave, tmask);
+#ifdef RTC_DIAG
+                const unsigned long long dt0 = __builtin_amdgcn_s_memtime();
+#endif
+                c = closest_hit<SPHERES>(P, pos, dir, primaryWave, tmask, lds);
+#ifdef RTC_DIAG
+                diagTrace += __builtin_amdgcn_s_memtime() - dt0;
+#endif
                 segTraced++;
                 segTests += primaryWave ? listLen : (unsigned)P.triCount;
             }
@@ -851,11 +947,304 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     if (g_rtc_diag && lane == 0) {
         const int wave = threadIdx.x >> 6;
         const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
-        g_rtc_diag[3 * w] = __builtin_amdgcn_s_memtime() - diagT0;
-        g_rtc_diag[3 * w + 1] = diagIters;
-        g_rtc_diag[3 * w + 2] = diagT0;
+        g_rtc_diag[4 * w] = __builtin_amdgcn_s_memtime() - diagT0;
+        g_rtc_diag[4 * w + 1] = diagIters;
+        g_rtc_diag[4 * w + 2] = diagT0;
+        g_rtc_diag[4 * w + 3] = diagTrace;
     }
 #endif
+    if (P.segments) {
+        unsigned long long a = segCalls, b = segTraced, n = segTests;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+            n += __shfl_xor(n, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.segments[0], a);
+            atomicAdd(&P.segments[1], b);
+            atomicAdd(&P.segments[2], n);
+        }
+    }
+}
+
+/* ---- the fused launch: cooperative heavy tiles + sky tiles ------------------------------------------------
+ * A 1920x1080 frame of ultracomplex.obj has ~1.3 k tiles (of 32.6 k) whose pixels see geometry.  Those "heavy"
+ * tiles run 128+ segment iterations of full 120-triangle tests plus Box-Muller shading per lane, while a sky
+ * tile is 64 environment lookups; with one lane per pixel the heavy waves alone set the frame time (a few
+ * of them per SIMD, latency-bound, long after the sky waves finished).  In the fused launch every heavy tile
+ * gets a whole workgroup and kCoop = 4 lanes per pixel:
+ *   - the lanes of a pixel hold identical state (RNG, ray, throughput, sample count) and split each
+ *     calculateRayCollision: lane j tests triangles j, j+4, ... (primary segments: the tile's candidates
+ *     j, j+4, ... in index order), then an exact (dst, index) lexicographic min across the 4 lanes -- the
+ *     reference keeps the first of equal distances (strict `<`, raytracing.c:231), i.e. the lowest index;
+ *   - RandomDiretion's three Box-Muller normals (moremath.c:97-108) are evaluated one per lane (every lane
+ *     advances the RNG through all six draws; lane j keeps draws 2j, 2j+1) and gathered by shuffles;
+ *   - the environment's two powf calls (raytracing.c:153,155) are evaluated one per lane and gathered.
+ * Every value is produced by the same operations as in rtc_render_kernel, only on different lanes, so the
+ * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
+ * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
+constexpr int kCoop = 4;
+constexpr int kCoopMaxTris = kLdsTris; /* scene and candidate records in LDS: 32 KB per heavy workgroup */
+
+__global__ __launch_bounds__(1024) void rtc_order_fused(const unsigned *__restrict__ tileW, int numTiles, int numBlocks,
+                                                         int *__restrict__ order)
+{
+    __shared__ int cnt[65];
+    __shared__ int heavy;
+    if (threadIdx.x < 65)
+        cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
+        if (tileW[i] > 0)
+            atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1); /* bucket 0 = 64 heavy pixels */
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int b = 0; b < 64; ++b) {
+            const int c = cnt[b];
+            cnt[b] = off;
+            off += c;
+        }
+        heavy = off;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
+        if (tileW[i] > 0)
+            order[atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1)] = i;
+    const int H = heavy;
+    for (int b = threadIdx.x; b < numBlocks; b += blockDim.x)
+        order[H + b] = -(b + 2);
+    for (int i = H + numBlocks + threadIdx.x; i < numTiles + numBlocks; i += blockDim.x)
+        order[i] = -1;
+}
+
+/* Cooperative calculateRayCollision for the kCoop lanes of one pixel (no spheres in the fused launch).
+ * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
+ * lane `sub` of a group reads record sub, sub+4, ... (four distinct records per wave instruction, each
+ * broadcast to 16 lanes). */
+__device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 dir, bool primarySeg,
+                                              const DevTri *__restrict__ sTri, const DevPrimF *__restrict__ sPrimF,
+                                              const int *__restrict__ sCand, int L, int sub)
+{
+    Closest c{999999.f, -1};
+    if (primarySeg) {
+        for (int k = sub; k < L; k += kCoop)
+            primary_test(P, dir, sPrimF[k], sCand[k], 0, c);
+    } else {
+#pragma unroll 2
+        for (int t = sub; t < P.triPadded; t += kCoop)
+            general_test(pos, dir, sTri[t], t, c);
+    }
+#pragma unroll
+    for (int k = 1; k < kCoop; k <<= 1) {
+        const float od = __shfl_xor(c.dst, k);
+        const int oi = __shfl_xor(c.idx, k);
+        if (od < c.dst || (od == c.dst && (unsigned)oi < (unsigned)c.idx)) {
+            c.dst = od;
+            c.idx = oi;
+        }
+    }
+    return c;
+}
+
+/* RandomDiretion (moremath.c:104-108) with the three normals on three lanes of the pixel's group */
+__device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int groupBase)
+{
+    const int mine = sub < 3 ? sub : 0;
+    float uTheta = 0.f, uRho = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float a = random_value(s);
+        const float b = random_value(s);
+        if (k == mine) {
+            uTheta = a;
+            uRho = b;
+        }
+    }
+    /* RandomValueNormalDistrubtion (moremath.c:97-102) */
+    const float theta = (float)(2 * 3.14159265 * (double)uTheta);
+    const float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)uRho));
+    const float n = (float)((double)rho * rtcmath::cos((double)theta));
+    const float nx = __shfl(n, groupBase), ny = __shfl(n, groupBase + 1), nz = __shfl(n, groupBase + 2);
+    return normalized(V3{nx, ny, nz});
+}
+
+/* getEnvironmentLight (raytracing.c:151-160) with its two powf calls on two lanes of the pixel's group */
+__device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub, int groupBase)
+{
+    const float sky = smoothstep(0.f, 0.74f, -dir.y);
+    const float sunDot = fmaxf(0.f, dot(dir, s.sun));
+    const bool second = (sub & 1) != 0;
+    const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f);
+    const float skyGradientT = __shfl(pw, groupBase);
+    const float sunPow = __shfl(pw, groupBase + 1);
+    const V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
+    const float sun = sunPow * s.intensity;
+    const float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
+    const float sunMask = dir.y < 0.f ? 1.f : 0.f;
+    const float sv = sun * sunMask;
+    return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
+}
+
+#ifndef RTC_FUSED_WAVES
+#define RTC_FUSED_WAVES 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_FUSED_WAVES))) void rtc_render_fused(
+    RenderParams P, const unsigned *__restrict__ tileW)
+{
+    __shared__ DevTri sTri[kLdsTris];
+    __shared__ DevPrimF sPrimF[kLdsTris];
+    __shared__ int sCand[kLdsTris];
+    __shared__ int sCount;
+    const int item = P.order[blockIdx.x];
+    if (item == -1)
+        return;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    unsigned segCalls = 0, segTraced = 0;
+    unsigned long long segTests = 0;
+    if (item < -1) {
+        /* ---- sky block: 4 tiles, one wave each; heavy tiles are rendered by their own workgroup ---- */
+        const int b = -item - 2;
+        const int bx = b % P.blocksX, by = b / P.blocksX;
+        const int tile = (by * 2 + (wave >> 1)) * (P.blocksX * 2) + bx * 2 + (wave & 1);
+        if (tileW[__builtin_amdgcn_readfirstlane(tile)] > 0)
+            return;
+        const PixelRay px = pixel_ray(P, bx, by);
+        V3 acc{0.f, 0.f, 0.f};
+        if (px.valid && P.spp > 0 && P.maxBounce > 0) {
+            /* see the skyTile path of rtc_render_kernel */
+#pragma unroll 2
+            for (int s = 0; s < P.spp; ++s) {
+                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
+                acc = add(acc, mul(l, P.invSpp));
+            }
+            segCalls = (unsigned)P.spp;
+            segTraced = P.hoist ? 1u : (unsigned)P.spp;
+        }
+        if (px.valid) {
+            const size_t o = (size_t)px.r * (size_t)P.width + (size_t)px.x;
+            P.colors[3 * o] = float_to_u8(acc.x);
+            P.colors[3 * o + 1] = float_to_u8(acc.y);
+            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (P.accum) {
+                P.accum[3 * o] = acc.x;
+                P.accum[3 * o + 1] = acc.y;
+                P.accum[3 * o + 2] = acc.z;
+            }
+        }
+    } else {
+        /* ---- heavy tile: 4 waves x 16 pixels x kCoop lanes ---- */
+        const int tile = item;
+        const int tilesX = P.blocksX * 2;
+        const int tx = tile % tilesX, ty = tile / tilesX;
+        const int sub = lane & (kCoop - 1);
+        const int groupBase = lane & ~(kCoop - 1);
+        const int pi = wave * (64 / kCoop) + lane / kCoop; /* pixel of the 8x8 tile, row-major */
+        const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
+        const bool valid = x < P.width && r < P.rows;
+        const int y = P.rowStart + r * P.rowStride;
+        const V3 pdir = primary_dir(P, x, y);
+        /* LDS: the scene's records, the tile's primary candidates (index order) and their records */
+        for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
+            sTri[i] = P.tris[i];
+        if (wave == 0) {
+            const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
+            int base = 0;
+            for (int w = 0; w < P.maskWords; ++w) {
+                const unsigned long long m = mask[w];
+                if ((m >> lane) & 1ull)
+                    sCand[base + __popcll(m & ((1ull << lane) - 1ull))] = w * 64 + lane;
+                base += __popcll(m);
+            }
+            if (lane == 0)
+                sCount = base;
+        }
+        __syncthreads();
+        const unsigned L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
+        for (int k = threadIdx.x; k < (int)L; k += kBlock)
+            sPrimF[k] = P.primF[sCand[k]];
+        __syncthreads();
+
+        unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
+        V3 acc{0.f, 0.f, 0.f};
+        bool alive = valid && P.spp > 0 && P.maxBounce > 0;
+        int sample = 0, bounce = 0;
+        V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+        Closest primary{999999.f, -1};
+        if (P.hoist && alive) {
+            primary = coop_trace(P, pos, dir, true, sTri, sPrimF, sCand, (int)L, sub);
+            segTraced++;
+            segTests += L;
+        }
+        while (__any(alive)) {
+            if (alive) {
+                Closest c;
+                segCalls++;
+                if (P.hoist && bounce == 0) {
+                    c = primary;
+                } else {
+                    c = coop_trace(P, pos, dir, bounce == 0, sTri, sPrimF, sCand, (int)L, sub);
+                    segTraced++;
+                    segTests += bounce == 0 ? L : (unsigned)P.triCount;
+                }
+                bool endSample;
+                if (c.idx >= 0) {
+                    /* calcColor hit branch, raytracing.c:272-287 */
+                    const V3 hitPoint = add(pos, mul(dir, c.dst));
+                    const DevTri T = P.tris[c.idx];
+                    const DevMat M = P.mats[c.idx];
+                    const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
+                    const V3 diffuseDir = normalized(add(normal, random_direction_coop(rng, sub, groupBase)));
+                    const V3 specularDir = reflect(dir, normal);
+                    dir = lerp(diffuseDir, specularDir, M.smoothness);
+                    pos = hitPoint;
+                    const V3 emitted = mul(color, M.emission);
+                    light = add(light, mulv(emitted, rayColor));
+                    rayColor = mulv(rayColor, color);
+                    const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                    endSample = p < random_value(rng);
+                    if (!endSample) {
+                        rayColor = mul(rayColor, 1.f / p);
+                        bounce++;
+                        endSample = bounce >= P.maxBounce;
+                    }
+                } else {
+                    light = add(light, mulv(environment_coop(dir, P.env, sub, groupBase), rayColor));
+                    endSample = true;
+                }
+                if (endSample) {
+                    acc = add(acc, mul(light, P.invSpp)); /* main.c:99 */
+                    sample++;
+                    if (sample >= P.spp) {
+                        alive = false;
+                    } else {
+                        pos = P.origin;
+                        dir = pdir;
+                        rayColor = V3{1.f, 1.f, 1.f};
+                        light = V3{0.f, 0.f, 0.f};
+                        bounce = 0;
+                    }
+                }
+            }
+        }
+        if (valid && sub == 0) {
+            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
+            P.colors[3 * o] = float_to_u8(acc.x);
+            P.colors[3 * o + 1] = float_to_u8(acc.y);
+            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (P.accum) {
+                P.accum[3 * o] = acc.x;
+                P.accum[3 * o + 1] = acc.y;
+                P.accum[3 * o + 2] = acc.z;
+            }
+        }
+        if (sub != 0) {
+            segCalls = segTraced = 0;
+            segTests = 0;
+        }
+    }
     if (P.segments) {
         unsigned long long a = segCalls, b = segTraced, n = segTests;
         for (int off = 32; off > 0; off >>= 1) {
@@ -930,14 +1319,18 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     hipStream_t st = (hipStream_t)stream;
     P.primF = s->primF;
     P.primX = s->primX;
-    /* tile candidate lists (one bit-set per 8x8 tile, 4 per workgroup), workgroup weights and the dispatch
-     * order, in one scratch buffer grown on demand (hipFree synchronises, so a previous launch still reading
-     * the old buffer has finished) */
-    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords > 0;
-    const size_t blocks = (size_t)grid.x * grid.y;
-    const size_t maskBytes = blocks * 4 * (size_t)s->maskWords * sizeof(unsigned long long);
+    /* tile candidate lists (one bit-set per 8x8 tile, 4 per workgroup), workgroup and tile weights and the
+     * dispatch order, in one scratch buffer grown on demand (hipFree synchronises, so a previous launch still
+     * reading the old buffer has finished) */
+    const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
+    /* (a scene without triangles culls too: every tile is then a sky tile) */
+    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL);
+    const bool fused = cull && !debug && P.sphereCount == 0 && s->triPadded <= kCoopMaxTris &&
+                       !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
+    const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
+    const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     if (cull) {
-        const size_t need = maskBytes + 2 * blocks * sizeof(int);
+        const size_t need = maskBytes + (blocks + tiles + tiles + blocks) * sizeof(int);
         if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (ms->scratch)
@@ -948,19 +1341,28 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             ms->scratchCap = need;
         }
     }
+    P.blocksX = (int)grid.x;
     if (s->triPadded > 0)
-        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 63) / 64), dim3(64), 0, st, s->tris, s->primF,
-                           s->primX, s->triPadded, P.origin);
+        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
+                           s->primF, s->primX, s->triPadded + 8, P.origin);
     if (cull) {
         unsigned long long *mask = (unsigned long long *)s->scratch;
         unsigned *weight = (unsigned *)(s->scratch + maskBytes);
-        int *order = (int *)(s->scratch + maskBytes + blocks * sizeof(int));
-        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight);
-        hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
+        unsigned *tileW = weight + blocks;
+        int *order = (int *)(tileW + tiles);
+        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW);
         P.tileMask = mask;
+        if (fused) {
+            hipLaunchKernelGGL(rtc_order_fused, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, (int)blocks, order);
+            P.order = order;
+            hipLaunchKernelGGL(rtc_render_fused, dim3((unsigned)(tiles + blocks)), dim3(kBlock), 0, st, P,
+                               (const unsigned *)tileW);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
+        hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
         P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
     }
-    const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     if (P.sphereCount > 0 && debug)
         hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, st, P);
     else if (P.sphereCount > 0)

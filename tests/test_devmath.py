@@ -39,3 +39,11 @@ def test_devmath_matches_glibc_where_it_matters(checker):
         n, vs_glibc, vs_cr = map(int, m.groups())
         assert vs_cr <= n * 1e-7  # same correctly-rounded result as the double-glibc evaluation
         assert vs_glibc <= n * 1e-3  # glibc powf itself is within 0.82 ulp, not correctly rounded
+    # the device's powf: glibc's own algorithm (FMA build), bit for bit against libm's powf
+    for y in ("0.35", "22", "7.5", "1.3", "0.5"):
+        m = re.search(rf"glibc-powf y={y}: (\d+) inputs, fma-build (\d+) != libm", out)
+        assert m and int(m.group(1)) > 4_000_000 and int(m.group(2)) == 0, out
+    m = re.search(r"glibc-powf random: (\d+) inputs, fma-build (\d+) != libm", out)
+    assert m and int(m.group(2)) == 0, out
+    m = re.search(r"random_value: (\d+) != divide", out)
+    assert m and int(m.group(1)) == 0, out

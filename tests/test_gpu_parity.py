@@ -136,6 +136,13 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
     assert np.array_equal(_bits(a0), _bits(a1)) and np.array_equal(c0, c1)
     assert s0["segments"] == s1["segments"]
     assert s1["tri_tests"] <= s0["tri_tests"]
+    # one lane per pixel (RTC_F_NO_COOP) == 4 cooperating lanes per pixel in tiles that see geometry
+    c2, a2, s2 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "coop": False}),
+                           want_accum=True)
+    assert np.array_equal(_bits(a1), _bits(a2)) and np.array_equal(c1, c2)
+    # (primary segments always visit only the candidates in the cooperative path, even when other pixels of
+    # the wave are on later bounces: fewer tests)
+    assert s1["segments"] == s2["segments"] and s1["tri_tests"] <= s2["tri_tests"]
     print(f"{name} hoist={hoist}: tests {s0['tri_tests']} -> {s1['tri_tests']}")
 
 

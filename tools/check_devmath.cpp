@@ -61,5 +61,43 @@ int main(int argc, char **argv)
         }
         printf("pow y=%g: %lld inputs, %lld != glibc powf, %lld != double-glibc exp2(y*log2 x)\n", y, n3, dglibc, dcr);
     }
+    // 4. the restated glibc powf (FMA build and plain build) against libm's own powf, every float x in [0, 1]
+    const float ys2[5] = {0.35f, 22.f, 7.5f, 1.3f, 0.5f};
+    for (float y : ys2) {
+        long long n4 = 0, dfma = 0, dplain = 0;
+#pragma omp parallel for reduction(+ : n4, dfma, dplain) schedule(static, 65536)
+        for (long long b = 0; b <= 0x3f800000LL; b += stride) {
+            const float x = f_of((uint32_t)b);
+            const uint32_t g = rtcmath::f2u(powf(x, y));
+            n4++;
+            dfma += rtcmath::f2u(rtcmath::powf_glibc<true>(x, y)) != g;
+            dplain += rtcmath::f2u(rtcmath::powf_glibc<false>(x, y)) != g;
+        }
+        printf("glibc-powf y=%g: %lld inputs, fma-build %lld != libm, plain-build %lld != libm\n", y, n4, dfma, dplain);
+    }
+    // 4b. RandomValue's divide-free form (rtc_device.h random_value) on every u32
+    {
+        long long dr = 0;
+#pragma omp parallel for reduction(+ : dr) schedule(static, 1 << 20)
+        for (long long r = 0; r <= 0xffffffffLL; r += stride) {
+            const float a = (float)((double)r / 4294967295.0);
+            const float b = (float)fma((double)r, 0x1p-64, (double)r * 0x1p-32);
+            dr += (a != b);
+        }
+        printf("random_value: %lld != divide\n", dr);
+    }
+    // 5. random (x, y) over the whole float range (both signs, subnormals, inf, NaN): bits compared, NaN == NaN
+    {
+        long long n5 = 0, d5 = 0;
+        uint64_t s = 0x9e3779b97f4a7c15ull;
+        for (long long k = 0; k < 20000000 / (long long)stride + 1000; ++k) {
+            s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+            const float x = f_of((uint32_t)s), y = (k & 1) ? f_of((uint32_t)(s >> 32)) : (float)(int)((s >> 40) % 64) - 31.f;
+            const float g = powf(x, y), a = rtcmath::powf_glibc<true>(x, y);
+            n5++;
+            d5 += !((g != g && a != a) || rtcmath::f2u(g) == rtcmath::f2u(a));
+        }
+        printf("glibc-powf random: %lld inputs, fma-build %lld != libm\n", n5, d5);
+    }
     return 0;
 }

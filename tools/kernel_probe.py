@@ -37,6 +37,7 @@ if not DIAG:
         "faithful": (tris, rt.RenderConfig(W, H, SPP, 10, True)),
         "faithful_nocull": (tris, rt.RenderConfig(W, H, SPP, 10, True, tile_cull=False)),
         "faithful_raster": (tris, rt.RenderConfig(W, H, SPP, 10, True, reorder=False)),
+        "faithful_nocoop": (tris, rt.RenderConfig(W, H, SPP, 10, True, coop=False)),
         "hoist": (tris, rt.RenderConfig(W, H, SPP, 10, True, hoist=True)),
         "mb1": (tris, rt.RenderConfig(W, H, SPP, 1, True)),
         "mb1_hoist": (tris, rt.RenderConfig(W, H, SPP, 1, True, hoist=True)),
@@ -46,7 +47,7 @@ if not DIAG:
         "spp16": (tris, rt.RenderConfig(W, H, 16, 10, True)),
     }
     if QUICK:
-        variants = {k: variants[k] for k in ("faithful", "faithful_nocull", "faithful_raster", "hoist", "mb1", "empty_scene")}
+        variants = {k: variants[k] for k in ("faithful", "faithful_nocull", "faithful_raster", "faithful_nocoop", "hoist", "mb1", "empty_scene")}
     for k, (t, cfg) in variants.items():
         st = timed(t, cfg)
         print(json.dumps({"variant": k, "T": len(t), "ms": round(st["render_ms"], 3), "segments": st["segments"], "tri_tests": st["tri_tests"],
@@ -55,12 +56,12 @@ else:
     for hoist, reorder in ((False, True), (False, False), (True, True)):
         cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, reorder=reorder)
         nw = ((W + 15) // 16) * ((H + 15) // 16) * 4
-        buf = torch.zeros(nw * 3, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(nw * 4, dtype=torch.int64, device="cuda")
         rt.lib().rtc_diag_set_buffer.argtypes = [C.c_void_p]
         rt.check(rt.lib().rtc_diag_set_buffer(C.c_void_p(buf.data_ptr())), "diag")
         _, _, st = rt.render(tris, None, scene, cam, cfg)
         torch.cuda.synchronize()
-        d = buf.view(nw, 3).cpu().numpy()
+        d = buf.view(nw, 4).cpu().numpy()
         cyc, it, t0 = d[:, 0].astype(np.float64), d[:, 1], d[:, 2]
         span = (t0 + d[:, 0]).max() - t0.min()
         q = lambda a, p: float(np.percentile(a, p))
@@ -71,5 +72,8 @@ else:
                           "memtime_span": float(span),
                           "share_waves_over_2x_median": float((cyc > 2 * np.median(cyc)).mean()),
                           "cycles_in_waves_over_2x_median": float(cyc[cyc > 2 * np.median(cyc)].sum() / cyc.sum()),
+                          "heavy_waves": int((it > 0).sum()),
+                          "heavy_trace_share": float(d[it > 0, 3].sum() / max(1.0, cyc[it > 0].sum())),
+                          "heavy_cycles_per_iter_p50": float(np.median(cyc[it > 0] / np.maximum(it[it > 0], 1))),
                           }), flush=True)
         np.save(os.path.join(REPO, "gpurun_out", f"wavecycles_hoist{int(hoist)}_reorder{int(reorder)}.npy"), d)
