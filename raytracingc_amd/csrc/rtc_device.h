@@ -77,19 +77,43 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
 /* powf for the environment (raytracing.c:153,155): glibc 2.35's own powf algorithm, tables and
  * coefficients, as its x86-64 FMA build evaluates it (rtc_math.h powf_glibc): bit-identical to the
  * reference's powf calls (tools/check_devmath.cpp: every float x in [0, 1] for the exponents checked). */
-__device__ __forceinline__ float pow_ref(float x, float y) { return rtcmath::powf_glibc<true>(x, y); }
-
 struct EnvParams {
     V3 sun, horizon, zenith, ground;
     float focus, intensity;
+    /* powf tables (null: glibc's constants in global memory; kernels point them at LDS copies) */
+    const double (*log2tab)[2];
+    const unsigned long long *exp2tab;
+};
+
+__device__ __forceinline__ float pow_ref(float x, float y, const EnvParams &s)
+{
+    return s.log2tab ? rtcmath::powf_glibc<true>(x, y, s.log2tab, s.exp2tab) : rtcmath::powf_glibc<true>(x, y);
+}
+
+/* The powf tables staged in LDS by a workgroup (call before its first __syncthreads) */
+struct PowTablesLds {
+    double log2tab[16][2];
+    unsigned long long exp2tab[32];
+    __device__ __forceinline__ void fill(int tid)
+    {
+        if (tid < 32)
+            log2tab[tid >> 1][tid & 1] = rtcmath::powf_data::kLog2Tab[tid >> 1][tid & 1];
+        else if (tid < 64)
+            exp2tab[tid - 32] = rtcmath::powf_data::kExp2Tab[tid - 32];
+    }
+    __device__ __forceinline__ void attach(EnvParams &e) const
+    {
+        e.log2tab = log2tab;
+        e.exp2tab = exp2tab;
+    }
 };
 
 /* getEnvironmentLight (raytracing.c:151-160) */
 __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
 {
-    float skyGradientT = pow_ref(smoothstep(0.f, 0.74f, -dir.y), 0.35f);
+    float skyGradientT = pow_ref(smoothstep(0.f, 0.74f, -dir.y), 0.35f, s);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
-    float sun = pow_ref(fmaxf(0.f, dot(dir, s.sun)), s.focus) * s.intensity;
+    float sun = pow_ref(fmaxf(0.f, dot(dir, s.sun)), s.focus, s) * s.intensity;
     float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
     float sunMask = dir.y < 0.f ? 1.f : 0.f;
     float sv = sun * sunMask;

@@ -288,14 +288,15 @@ RTC_HD int powf_checkint(unsigned iy)
 }
 RTC_HD bool powf_zeroinfnan(unsigned ix) { return 2 * ix - 1 >= 2u * 0x7f800000u - 1; }
 
-template <bool FMA> RTC_HD double powf_log2(unsigned ix) /* e_powf.c log2_inline */
+/* tables: glibc's by default; the device passes copies staged in LDS (same values) */
+template <bool FMA> RTC_HD double powf_log2(unsigned ix, const double (*tab)[2] = powf_data::kLog2Tab) /* e_powf.c log2_inline */
 {
     const unsigned tmp = ix - 0x3f330000u;
     const int i = (int)((tmp >> (23 - 4)) % 16);
     const unsigned top = tmp & 0xff800000u;
     const unsigned iz = ix - top;
     const int k = (int)top >> 23; /* arithmetic shift */
-    const double invc = powf_data::kLog2Tab[i][0], logc = powf_data::kLog2Tab[i][1];
+    const double invc = tab[i][0], logc = tab[i][1];
     const double z = (double)u2f(iz);
     const double r = mad<FMA>(z, invc, -1.0);
     const double y0 = logc + (double)k;
@@ -310,13 +311,15 @@ template <bool FMA> RTC_HD double powf_log2(unsigned ix) /* e_powf.c log2_inline
     return y;
 }
 
-template <bool FMA> RTC_HD float powf_exp2(double xd, unsigned signBias) /* e_powf.c exp2_inline */
+template <bool FMA>
+RTC_HD float powf_exp2(double xd, unsigned signBias,
+                       const unsigned long long *tab = powf_data::kExp2Tab) /* e_powf.c exp2_inline */
 {
     double kd = xd + powf_data::kExp2Shift;
     const unsigned long long ki = d2u(kd);
     kd -= powf_data::kExp2Shift;
     const double r = xd - kd;
-    unsigned long long t = powf_data::kExp2Tab[ki % 32];
+    unsigned long long t = tab[ki % 32];
     const unsigned long long ski = ki + signBias;
     t += ski << (52 - 5);
     const double s = u2d(t);
@@ -329,7 +332,9 @@ template <bool FMA> RTC_HD float powf_exp2(double xd, unsigned signBias) /* e_po
     return (float)y;
 }
 
-template <bool FMA> RTC_HD float powf_glibc(float x, float y) /* e_powf.c __powf, round-to-nearest */
+template <bool FMA>
+RTC_HD float powf_glibc(float x, float y, const double (*log2tab)[2] = powf_data::kLog2Tab,
+                        const unsigned long long *exp2tab = powf_data::kExp2Tab) /* e_powf.c __powf, round-to-nearest */
 {
     unsigned signBias = 0;
     unsigned ix = f2u(x), iy = f2u(y);
@@ -369,7 +374,7 @@ template <bool FMA> RTC_HD float powf_glibc(float x, float y) /* e_powf.c __powf
             ix -= 23u << 23;
         }
     }
-    const double logx = powf_log2<FMA>(ix);
+    const double logx = powf_log2<FMA>(ix, log2tab);
     const double ylogx = (double)y * logx;
     if ((d2u(ylogx) >> 47 & 0xffff) >= d2u(126.0) >> 47) {
         if (ylogx > 0x1.fffffffd1d571p+6)
@@ -377,7 +382,7 @@ template <bool FMA> RTC_HD float powf_glibc(float x, float y) /* e_powf.c __powf
         if (ylogx <= -150.0)
             return signBias ? -0.0f : 0.0f;
     }
-    return powf_exp2<FMA>(ylogx, signBias);
+    return powf_exp2<FMA>(ylogx, signBias, exp2tab);
 }
 
 /* powf(x, y) of raytracing.c:153,155 for x >= 0 (or NaN): exp2(y * log2(x)) in double, rounded once */

@@ -141,6 +141,10 @@ struct RtcDeviceScene {
     unsigned char *scratch;
     size_t scratchCap; /* bytes */
     int maskWords;     /* ceil(triPadded / 64) */
+    unsigned long long *segSlots; /* per-launch partial segment counters */
+    /* the split launch runs the sky kernel on `side`, concurrently with the heavy-tile kernel */
+    hipStream_t side;
+    hipEvent_t evFork, evJoin;
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -226,11 +230,22 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     if (e == hipSuccess)
         e = hipMalloc(&s->primX, dt.size() * sizeof(DevPrimX));
     if (e == hipSuccess)
+        e = hipMalloc(&s->segSlots, 256 * 16 * sizeof(unsigned long long));
+    if (e == hipSuccess)
         e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->mats, dm.data(), dm.size() * sizeof(DevMat), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->spheres, ds.data(), ds.size() * sizeof(DevSphere), hipMemcpyHostToDevice);
+    int leastPrio = 0, greatestPrio = 0;
+    if (e == hipSuccess)
+        e = hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio);
+    if (e == hipSuccess) /* the sky tiles yield to the heavy tiles */
+        e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, leastPrio);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
     if (e != hipSuccess) {
         rtc_scene_release(s);
         return rtc_fail(-(int)e, "scene upload failed: %s", hipGetErrorString(e));
@@ -258,6 +273,14 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->primX);
     if (s->scratch)
         (void)hipFree(s->scratch);
+    if (s->segSlots)
+        (void)hipFree(s->segSlots);
+    if (s->evFork)
+        (void)hipEventDestroy(s->evFork);
+    if (s->evJoin)
+        (void)hipEventDestroy(s->evJoin);
+    if (s->side)
+        (void)hipStreamDestroy(s->side);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -280,10 +303,12 @@ struct RenderParams {
     const DevPrimX *__restrict__ primX;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
+    int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter) */
     int blocksX; /* 16x16 blocks per row of the launch */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
+    unsigned long long *__restrict__ segSlots; /* kSegSlots x kSegSlotStride partial counters (flush_counters) */
     int triCount, triPadded, sphereCount, maskWords;
     int width, height, rows, rowStart, rowStride;
     int spp, maxBounce;
@@ -745,6 +770,54 @@ __global__ __launch_bounds__(1024) void rtc_order_blocks(const unsigned *__restr
         order[atomicAdd(&cnt[min(kOrderBuckets - 1, (int)((weight[i] + 15) / 16))], 1)] = i;
 }
 
+/* Segment counters.  One atomic per wave into the caller's three counters serialises in L2 (tens of
+ * thousands of same-address atomics per frame cost milliseconds), so waves add into kSegSlots slots, each
+ * in its own 128-B line, and rtc_reduce_segments folds the slots into the caller's counters at the end. */
+constexpr int kSegSlots = 256, kSegSlotStride = 16; /* u64 */
+static_assert(kSegSlots * kSegSlotStride == 256 * 16, "rtc_scene_upload allocates 256 x 16 u64");
+
+__device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned segCalls, unsigned segTraced,
+                                               unsigned long long segTests, int lane)
+{
+    if (!P.segments)
+        return;
+    unsigned long long a = segCalls, b = segTraced, n = segTests;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+        n += __shfl_xor(n, off);
+    }
+    if (lane == 0 && (a | b | n)) {
+        const unsigned slot = (blockIdx.x * 7u + blockIdx.y * 131u + (threadIdx.x >> 6)) % kSegSlots;
+        unsigned long long *c = P.segSlots + (size_t)slot * kSegSlotStride;
+        atomicAdd(&c[0], a);
+        atomicAdd(&c[1], b);
+        atomicAdd(&c[2], n);
+    }
+}
+
+__global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(const unsigned long long *__restrict__ slots,
+                                                                 unsigned long long *__restrict__ out)
+{
+    __shared__ unsigned long long part[3][kSegSlots / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long v = slots[(size_t)t * kSegSlotStride + k];
+        for (int off = 32; off > 0; off >>= 1)
+            v += __shfl_xor(v, off);
+        if (lane == 0)
+            part[k][w] = v;
+    }
+    __syncthreads();
+    if (t < 3) {
+        unsigned long long v = 0;
+        for (int i = 0; i < kSegSlots / 64; ++i)
+            v += part[t][i];
+        out[t] += v; /* stream-ordered after every render kernel of the launch: no atomic needed */
+    }
+}
+
 #ifdef RTC_DIAG
 /* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp, cycles inside
  * closest_hit} */
@@ -777,14 +850,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     const V3 pdir = px.dir;
     unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
 
-    /* general-path records in LDS (small scenes) */
+    /* general-path records in LDS (small scenes) and the powf tables */
     __shared__ DevTri sTris[kLdsTris];
+    __shared__ PowTablesLds sPow;
     const bool useLds = RTC_GEN_LDS && P.triPadded <= kLdsTris;
     if (useLds) {
         for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
             sTris[i] = P.tris[i];
-        __syncthreads();
     }
+    sPow.fill(threadIdx.x);
+    __syncthreads();
+    sPow.attach(P.env);
     const DevTri *lds = useLds ? sTris : nullptr;
 
     /* this wave's primary candidates (rtc_tile_cull) */
@@ -953,19 +1029,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
         g_rtc_diag[4 * w + 3] = diagTrace;
     }
 #endif
-    if (P.segments) {
-        unsigned long long a = segCalls, b = segTraced, n = segTests;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_xor(a, off);
-            b += __shfl_xor(b, off);
-            n += __shfl_xor(n, off);
-        }
-        if (lane == 0) {
-            atomicAdd(&P.segments[0], a);
-            atomicAdd(&P.segments[1], b);
-            atomicAdd(&P.segments[2], n);
-        }
-    }
+    flush_counters(P, segCalls, segTraced, segTests, lane);
 }
 
 /* ---- the fused launch: cooperative heavy tiles + sky tiles ------------------------------------------------
@@ -985,10 +1049,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
  * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
  * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
 constexpr int kCoop = 4;
-constexpr int kCoopMaxTris = kLdsTris; /* scene and candidate records in LDS: 32 KB per heavy workgroup */
+#ifndef RTC_SKY_UNROLL
+#define RTC_SKY_UNROLL 2
+#endif
+constexpr int kCoopMaxTris = kLdsTris; /* scene and candidate records in LDS: <= 33 KB per heavy workgroup */
 
-__global__ __launch_bounds__(1024) void rtc_order_fused(const unsigned *__restrict__ tileW, int numTiles, int numBlocks,
-                                                         int *__restrict__ order)
+__global__ __launch_bounds__(1024) void rtc_order_heavy(const unsigned *__restrict__ tileW, int numTiles,
+                                                         int *__restrict__ order, int *__restrict__ heavyOut)
 {
     __shared__ int cnt[65];
     __shared__ int heavy;
@@ -997,7 +1064,7 @@ __global__ __launch_bounds__(1024) void rtc_order_fused(const unsigned *__restri
     __syncthreads();
     for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
         if (tileW[i] > 0)
-            atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1); /* bucket 0 = 64 heavy pixels */
+            atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1); /* bucket 0 = 64 pixels with candidates */
     __syncthreads();
     if (threadIdx.x == 0) {
         int off = 0;
@@ -1012,12 +1079,14 @@ __global__ __launch_bounds__(1024) void rtc_order_fused(const unsigned *__restri
     for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
         if (tileW[i] > 0)
             order[atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1)] = i;
-    const int H = heavy;
-    for (int b = threadIdx.x; b < numBlocks; b += blockDim.x)
-        order[H + b] = -(b + 2);
-    for (int i = H + numBlocks + threadIdx.x; i < numTiles + numBlocks; i += blockDim.x)
+    for (int i = heavy + threadIdx.x; i < numTiles; i += blockDim.x)
         order[i] = -1;
+    if (threadIdx.x == 0) {
+        heavyOut[0] = heavy;
+        heavyOut[1] = 0;
+    }
 }
+
 
 /* Cooperative calculateRayCollision for the kCoop lanes of one pixel (no spheres in the fused launch).
  * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
@@ -1076,7 +1145,7 @@ __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int s
     const float sky = smoothstep(0.f, 0.74f, -dir.y);
     const float sunDot = fmaxf(0.f, dot(dir, s.sun));
     const bool second = (sub & 1) != 0;
-    const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f);
+    const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f, s);
     const float skyGradientT = __shfl(pw, groupBase);
     const float sunPow = __shfl(pw, groupBase + 1);
     const V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
@@ -1087,35 +1156,26 @@ __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int s
     return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
 }
 
-#ifndef RTC_FUSED_WAVES
-#define RTC_FUSED_WAVES 4
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_FUSED_WAVES))) void rtc_render_fused(
-    RenderParams P, const unsigned *__restrict__ tileW)
+/* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile of a 16x16 block; the waves of
+ * tiles with primary candidates return at once (rtc_render_heavy renders those).  Few registers, so many
+ * waves per SIMD hide the latency of the environment's double-precision chains. */
+__global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const unsigned *__restrict__ tileW)
 {
-    __shared__ DevTri sTri[kLdsTris];
-    __shared__ DevPrimF sPrimF[kLdsTris];
-    __shared__ int sCand[kLdsTris];
-    __shared__ int sCount;
-    const int item = P.order[blockIdx.x];
-    if (item == -1)
-        return;
+    __shared__ PowTablesLds sPow;
+    sPow.fill(threadIdx.x);
+    __syncthreads();
+    sPow.attach(P.env);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
     unsigned segCalls = 0, segTraced = 0;
-    unsigned long long segTests = 0;
-    if (item < -1) {
-        /* ---- sky block: 4 tiles, one wave each; heavy tiles are rendered by their own workgroup ---- */
-        const int b = -item - 2;
-        const int bx = b % P.blocksX, by = b / P.blocksX;
-        const int tile = (by * 2 + (wave >> 1)) * (P.blocksX * 2) + bx * 2 + (wave & 1);
-        if (tileW[__builtin_amdgcn_readfirstlane(tile)] > 0)
+    {
+        const int bx = blockIdx.x, by = blockIdx.y;
+        if (tileW[wave_tile(bx, by)] > 0)
             return;
         const PixelRay px = pixel_ray(P, bx, by);
         V3 acc{0.f, 0.f, 0.f};
         if (px.valid && P.spp > 0 && P.maxBounce > 0) {
             /* see the skyTile path of rtc_render_kernel */
-#pragma unroll 2
+#pragma unroll RTC_SKY_UNROLL
             for (int s = 0; s < P.spp; ++s) {
                 const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
                 acc = add(acc, mul(l, P.invSpp));
@@ -1134,9 +1194,50 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_FUSE
                 P.accum[3 * o + 2] = acc.z;
             }
         }
-    } else {
-        /* ---- heavy tile: 4 waves x 16 pixels x kCoop lanes ---- */
-        const int tile = item;
+    }
+    flush_counters(P, segCalls, segTraced, 0ull, lane);
+}
+
+/* Heavy tiles (rtc_render_heavy): a fixed set of persistent workgroups takes the heavy tiles one at a time,
+ * heaviest first (rtc_order_heavy), from a work counter, so the launch size does not depend on how many
+ * tiles see geometry.  Dynamic LDS: the scene's records, the tile's candidate records and indices
+ * (rtc_heavy_lds_bytes). */
+constexpr int kHeavyWorkers = 2048;
+__host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
+{
+    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(int)) + 16;
+}
+
+#ifndef RTC_HEAVY_WAVES
+#define RTC_HEAVY_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
+    RenderParams P)
+{
+    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
+    __shared__ PowTablesLds sPow;
+    DevTri *sTri = (DevTri *)sDyn;
+    DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
+    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
+    int &sCount = sCand[P.triPadded];
+    __shared__ int sItem;
+    sPow.fill(threadIdx.x);
+    sPow.attach(P.env);
+    for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
+        sTri[i] = P.tris[i];
+    const int lane = threadIdx.x & 63;
+    unsigned segCalls = 0, segTraced = 0;
+    unsigned long long segTests = 0;
+    const int heavy = P.heavy[0]; /* rtc_order_heavy: number of heavy tiles; P.heavy[1]: next slot */
+    for (;;) {
+        if (threadIdx.x == 0)
+            sItem = atomicAdd(&P.heavy[1], 1);
+        __syncthreads();
+        const int slot = __builtin_amdgcn_readfirstlane(sItem);
+        if (slot >= heavy)
+            break;
+        const int tile = P.order[slot];
+        const int wave = threadIdx.x >> 6;
         const int tilesX = P.blocksX * 2;
         const int tx = tile % tilesX, ty = tile / tilesX;
         const int sub = lane & (kCoop - 1);
@@ -1146,9 +1247,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_FUSE
         const bool valid = x < P.width && r < P.rows;
         const int y = P.rowStart + r * P.rowStride;
         const V3 pdir = primary_dir(P, x, y);
-        /* LDS: the scene's records, the tile's primary candidates (index order) and their records */
-        for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
-            sTri[i] = P.tris[i];
+        /* LDS: the tile's primary candidates (index order) and their records */
         if (wave == 0) {
             const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
             int base = 0;
@@ -1244,25 +1343,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_FUSE
             segCalls = segTraced = 0;
             segTests = 0;
         }
+        __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
     }
-    if (P.segments) {
-        unsigned long long a = segCalls, b = segTraced, n = segTests;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_xor(a, off);
-            b += __shfl_xor(b, off);
-            n += __shfl_xor(n, off);
-        }
-        if (lane == 0) {
-            atomicAdd(&P.segments[0], a);
-            atomicAdd(&P.segments[1], b);
-            atomicAdd(&P.segments[2], n);
-        }
-    }
+    flush_counters(P, segCalls, segTraced, segTests, lane);
 }
 
 static EnvParams env_of(const Scene &s)
 {
-    EnvParams e;
+    EnvParams e{};
     e.sun = V3{s.normalizedSunDirection.x, s.normalizedSunDirection.y, s.normalizedSunDirection.z};
     e.horizon = V3{s.skyColorHorizon.x, s.skyColorHorizon.y, s.skyColorHorizon.z};
     e.zenith = V3{s.skyColorZenith.x, s.skyColorZenith.y, s.skyColorZenith.z};
@@ -1296,6 +1384,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.colors = (unsigned char *)dColors;
     P.accum = dAccum;
     P.segments = dSegments;
+    P.segSlots = s->segSlots;
     P.triCount = s->triCount;
     P.triPadded = s->triPadded;
     P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
@@ -1330,7 +1419,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     if (cull) {
-        const size_t need = maskBytes + (blocks + tiles + tiles + blocks) * sizeof(int);
+        const size_t need = maskBytes + (blocks + tiles + tiles + blocks + 4) * sizeof(int);
         if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (ms->scratch)
@@ -1342,6 +1431,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         }
     }
     P.blocksX = (int)grid.x;
+    if (dSegments)
+        HIP_TRY(hipMemsetAsync(s->segSlots, 0, kSegSlots * kSegSlotStride * sizeof(unsigned long long), st));
+    auto finish = [&]() -> int {
+        if (dSegments) {
+            hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
+            HIP_TRY(hipGetLastError());
+        }
+        return 0;
+    };
     if (s->triPadded > 0)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
                            s->primF, s->primX, s->triPadded + 8, P.origin);
@@ -1353,12 +1451,29 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW);
         P.tileMask = mask;
         if (fused) {
-            hipLaunchKernelGGL(rtc_order_fused, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, (int)blocks, order);
+            /* sky tiles on the side stream, concurrently with the heavy tiles on `st`; `st` then waits for both */
+            int *heavy = order + tiles + blocks;
+            hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
             P.order = order;
-            hipLaunchKernelGGL(rtc_render_fused, dim3((unsigned)(tiles + blocks)), dim3(kBlock), 0, st, P,
-                               (const unsigned *)tileW);
+            P.heavy = heavy;
+#ifndef RTC_SIDE_STREAM
+#define RTC_SIDE_STREAM 1
+#endif
+            hipStream_t skyStream = RTC_SIDE_STREAM ? s->side : st;
+            if (RTC_SIDE_STREAM) {
+                HIP_TRY(hipEventRecord(s->evFork, st));
+                HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
+            }
+            hipLaunchKernelGGL(rtc_render_sky, grid, dim3(kBlock), 0, skyStream, P, (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
-            return 0;
+            if (RTC_SIDE_STREAM)
+                HIP_TRY(hipEventRecord(s->evJoin, s->side));
+            hipLaunchKernelGGL(rtc_render_heavy, dim3((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers)),
+                               dim3(kBlock), rtc_heavy_lds_bytes(s->triPadded), st, P);
+            HIP_TRY(hipGetLastError());
+            if (RTC_SIDE_STREAM)
+                HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
+            return finish();
         }
         hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
         P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
@@ -1372,7 +1487,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     else
         hipLaunchKernelGGL((rtc_render_kernel<false, false>), grid, dim3(kBlock), 0, st, P);
     HIP_TRY(hipGetLastError());
-    return 0;
+    return finish();
 }
 
 /* ---- row de-interleave after a gather (bytes) ----------------------------------------------------- */
@@ -1637,7 +1752,7 @@ __global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n,
     if (i >= n)
         return;
     Scene s = scenes[i];
-    EnvParams e;
+    EnvParams e{};
     e.sun = v3(s.normalizedSunDirection);
     e.horizon = v3(s.skyColorHorizon);
     e.zenith = v3(s.skyColorZenith);
