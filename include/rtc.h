@@ -61,6 +61,8 @@ typedef struct RtcRenderDesc {
                                     timing; the frame is identical) */
 #define RTC_F_NO_COOP       0x10 /* tiles that see geometry keep one lane per pixel instead of a workgroup
                                     with 4 cooperating lanes per pixel (A/B timing; the frame is identical) */
+#define RTC_F_NO_CLUSTER_CULL 0x20 /* bounce rays of the cooperative path test every triangle instead of only
+                                      the clusters their half-line may reach (A/B timing; identical frame) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */
@@ -68,6 +70,7 @@ typedef struct RtcStats {
     unsigned long long segments; /* closest-hit queries traced (calculateRayCollision calls) */
     unsigned long long samples;  /* camera samples = pixels * spp */
     unsigned long long triTests; /* ray-triangle tests evaluated (segments x triangles the segment visits) */
+    unsigned long long clusterTests; /* ray-cluster bounding-ball tests (cooperative path, bounce rays) */
 } RtcStats;
 
 /* ---- error codes ----------------------------------------------------------------------------------- */
@@ -129,7 +132,7 @@ int rtc_rows_selected(const RtcRenderDesc *d);
  * rows_selected*width*3 bytes; dAccum: nullable device float buffer rows_selected*width*3; dSegments:
  * nullable device u64[RTC_SEGMENT_COUNTERS] the kernel atomically adds to: [0] calculateRayCollision calls
  * (the reference's segment count), [1] closest-hit queries actually traced (smaller with
- * RTC_F_HOIST_PRIMARY), [2] ray-triangle tests evaluated, [3] reserved.
+ * RTC_F_HOIST_PRIMARY), [2] ray-triangle tests evaluated, [3] ray-cluster bounding-ball tests.
  * A scene handle serves one stream at a time: its per-launch scratch (primary-ray records, tile candidate
  * lists) is rewritten by every launch. */
 #define RTC_SEGMENT_COUNTERS 4
@@ -150,6 +153,12 @@ int rtc_probe_ray_sphere(const Ray *rays, const Sphere *spheres, size_t n, int *
 int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *out);                  /* raytracing.c:151 */
 int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
                      vec3 *direction);                                                                  /* moremath.c:89-108 */
+/* Soundness probe of the bounce-ray cluster culling (no reference counterpart; raytracing.c:186-214 is the
+ * per-triangle test it must never contradict): clusters `tris` as rtc_scene_upload does and, for every ray,
+ * counts [0] hits inside clusters the ray was culled from (0 when sound), [1] clusters culled, [2] cluster
+ * tests, [3] hits, [4] float bits of the largest hit-point excess over a cluster's bounding radius. */
+int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
+                            unsigned long long counts[5]);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,7 @@ from ._abi import (  # noqa: F401
     RAY_DT,
     RTC_F_DEBUG_BOUNCES,
     RTC_F_HOIST_PRIMARY,
+    RTC_F_NO_CLUSTER_CULL,
     RTC_F_NO_COOP,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
@@ -132,11 +133,12 @@ class RenderConfig:
     tile_cull: bool = True  # primary segments visit their 8x8 tile's candidate triangles (bit-exact)
     reorder: bool = True  # dispatch the workgroups that see geometry first (same frame)
     coop: bool = True  # tiles that see geometry: 4 cooperating lanes per pixel (same frame)
+    cluster_cull: bool = True  # bounce rays skip triangle clusters they provably miss (same frame)
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
-                | (0 if self.coop else RTC_F_NO_COOP))
+                | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
@@ -168,7 +170,8 @@ def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, devic
     check(lib().rtc_render(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), device,
                            _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render")
     return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples, "tri_tests": st.triTests}
+                           "samples": st.samples, "tri_tests": st.triTests,
+                           "cluster_tests": st.clusterTests}
 
 
 def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, num_devices: int,
@@ -183,7 +186,8 @@ def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig,
     check(lib().rtc_render_multi(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), num_devices,
                                  _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render_multi")
     return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples, "tri_tests": st.triTests}
+                           "samples": st.samples, "tri_tests": st.triTests,
+                           "cluster_tests": st.clusterTests}
 
 
 class DeviceScene:
@@ -288,3 +292,14 @@ def random_sequences(seeds: np.ndarray, draws: int):
     d = np.zeros((n, draws, 3), np.float32)
     check(lib().rtc_probe_random(_ptr(sd), n, draws, _ptr(u), _ptr(g), _ptr(d)), "rtc_probe_random")
     return u, g, d
+
+
+def cluster_bound_probe(tris: np.ndarray, rays: np.ndarray) -> dict:
+    """Soundness of the bounce-ray cluster culling on the GPU (rtc_probe_cluster_bound): hits inside culled
+    clusters (must be 0), clusters culled, cluster tests, hits, largest hit excess over a bounding radius."""
+    t = np.ascontiguousarray(tris, TRIANGLE_DT)
+    r = np.ascontiguousarray(rays, RAY_DT)
+    c = np.zeros(5, np.uint64)
+    check(lib().rtc_probe_cluster_bound(_ptr(t), len(t), _ptr(r), len(r), _ptr(c)), "rtc_probe_cluster_bound")
+    return {"violations": int(c[0]), "culled": int(c[1]), "tests": int(c[2]), "hits": int(c[3]),
+            "max_excess": float(np.array([c[4]], np.uint64).astype(np.uint32).view(np.float32)[0])}

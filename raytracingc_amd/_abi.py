@@ -71,6 +71,7 @@ class RtcStats(C.Structure):
         ("segments", C.c_ulonglong),
         ("samples", C.c_ulonglong),
         ("triTests", C.c_ulonglong),
+        ("clusterTests", C.c_ulonglong),
     ]
 
 
@@ -79,6 +80,7 @@ RTC_F_DEBUG_BOUNCES = 0x2
 RTC_F_NO_TILE_CULL = 0x4
 RTC_F_NO_REORDER = 0x8
 RTC_F_NO_COOP = 0x10
+RTC_F_NO_CLUSTER_CULL = 0x20
 RTC_SEGMENT_COUNTERS = 4  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
@@ -115,6 +117,7 @@ EXPORTS = [
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async",
     "rtc_deinterleave_async",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
+    "rtc_probe_cluster_bound",
 ]
 
 _lib = None
@@ -169,6 +172,7 @@ def lib() -> C.CDLL:
     L.rtc_probe_ray_sphere.argtypes = [vp, vp, sz, vp, vp, vp]
     L.rtc_probe_environment.argtypes = [vp, vp, sz, vp]
     L.rtc_probe_random.argtypes = [vp, sz, ip, vp, vp, vp]
+    L.rtc_probe_cluster_bound.argtypes = [vp, ip, vp, sz, vp]
     _lib = L
     return L
 

@@ -17,7 +17,9 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -128,9 +130,32 @@ struct __attribute__((aligned(64))) DevPrimX {
     float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, q0x, q0y, q0z, dac0, pad[3];
 };
 
+/* ---- triangle clusters for bounce rays (the cooperative heavy-tile path) ------------------------------
+ * The triangles are grouped into clusters of kClusterSize (spatial median splits, rtc_build_clusters); a
+ * bounce ray skips a whole cluster when its half-line provably passes farther from the cluster's bounding
+ * ball than any point rayTriangle could report.  Bound (SURVEY Appendix A arithmetic, unit roundoff
+ * u = 2^-24): for a reported hit (|det| >= EPSILON, u, v in the triangle, dst >= EPSILON) the exact point
+ * pos + dst*dir lies within
+ *     eps = rho * (alpha + beta * S) + gamma * (S + E)
+ * of the triangle, where rho >= |dir|, S >= |pos - A|, E = the cluster's longest AB / AC edge, and
+ *     beta = F k 45 u E^2 / EPSILON,  alpha = F k 32 u E^3 / EPSILON,  k = 1 / (1 - 8 u E^2 rhoMax / EPSILON)
+ * (forward error of the f32 cross / dot products over the Cramer solution, divided by |det| >= EPSILON;
+ * safety factor F = 4; gamma covers the f32 evaluation of the cull test itself).  Clusters with
+ * 8 u E^2 rhoMax / EPSILON >= 1/2, and rays with |dir|_1 > rhoMax, are never culled. */
+constexpr int kClusterSize = 8;
+constexpr float kClusterRhoMax = 4.f;
+constexpr float kClusterGamma = 2e-5f;
+struct __attribute__((aligned(32))) DevCluster {
+    float cx, cy, cz, r;          /* bounding ball (every vertex A, A+AB, A+AC of the cluster inside) */
+    float alpha, beta, gammaE, e; /* the eps terms above: alpha, beta, gamma*E (or +inf: never cull), E */
+};
+
 struct RtcDeviceScene {
     int device;
     int triCount, triPadded, sphereCount; /* triPadded: multiple of kUnroll, zero (never-hit) records */
+    int clusterCount;   /* ceil(triCount / kClusterSize) */
+    DevTri *clTris;     /* clusterCount * kClusterSize records in cluster order, pad0 = reference index (int) */
+    DevCluster *clusters;
     DevTri *tris;
     DevMat *mats;
     DevSphere *spheres;
@@ -195,6 +220,112 @@ static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, in
     }
 }
 
+/* Clusters of kClusterSize triangles: recursive splits of the centroids along their longest extent, each
+ * split at a multiple of kClusterSize so that every leaf but the last is full (ceil(n / 8) clusters). */
+static void split_clusters(const std::vector<DevTri> &dt, std::vector<int> &idx, size_t lo, size_t hi)
+{
+    const size_t n = hi - lo;
+    if (n <= (size_t)kClusterSize)
+        return;
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    auto centroid = [&](int i, int a) {
+        const DevTri &t = dt[i];
+        const double A[3] = {t.ax, t.ay, t.az}, B[3] = {t.abx, t.aby, t.abz}, C[3] = {t.acx, t.acy, t.acz};
+        return A[a] + (B[a] + C[a]) / 3.0;
+    };
+    for (size_t k = lo; k < hi; ++k)
+        for (int a = 0; a < 3; ++a) {
+            const double c = centroid(idx[k], a);
+            if (c == c) {
+                mn[a] = std::min(mn[a], c);
+                mx[a] = std::max(mx[a], c);
+            }
+        }
+    int axis = 0;
+    for (int a = 1; a < 3; ++a)
+        if (mx[a] - mn[a] > mx[axis] - mn[axis])
+            axis = a;
+    std::stable_sort(idx.begin() + lo, idx.begin() + hi, [&](int p, int q) {
+        const double cp = centroid(p, axis), cq = centroid(q, axis);
+        return (cp == cp ? cp : 1e300) < (cq == cq ? cq : 1e300);
+    });
+    const size_t leaves = (n + kClusterSize - 1) / kClusterSize;
+    const size_t mid = lo + (leaves + 1) / 2 * kClusterSize;
+    split_clusters(dt, idx, lo, mid);
+    split_clusters(dt, idx, mid, hi);
+}
+
+static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std::vector<DevTri> &ct,
+                               std::vector<DevCluster> &cl)
+{
+    const int nc = (triCount + kClusterSize - 1) / kClusterSize;
+    std::vector<int> idx(triCount);
+    for (int i = 0; i < triCount; ++i)
+        idx[i] = i;
+    split_clusters(dt, idx, 0, (size_t)triCount);
+    ct.assign((size_t)nc * kClusterSize, DevTri{});
+    cl.assign((size_t)(nc > 0 ? nc : 1), DevCluster{});
+    const double u = 0x1p-24, eps = 0.001; /* |det| >= 0.001f > 0.001 for every reported hit */
+    for (int c = 0; c < nc; ++c) {
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, E = 0.0;
+        bool finite = true;
+        const int n = std::min(kClusterSize, triCount - c * kClusterSize);
+        for (int j = 0; j < kClusterSize; ++j) {
+            DevTri &r = ct[(size_t)c * kClusterSize + j];
+            if (j >= n) { /* zero record: never hit; index -1 */
+                const int none = -1;
+                memcpy(&r.pad0, &none, sizeof none);
+                continue;
+            }
+            const int i = idx[(size_t)c * kClusterSize + j];
+            r = dt[i];
+            memcpy(&r.pad0, &i, sizeof i);
+            const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
+            for (int a = 0; a < 3; ++a) {
+                const double v[3] = {A[a], A[a] + B[a], A[a] + C[a]};
+                for (double x : v) {
+                    finite = finite && std::isfinite(x);
+                    lo[a] = std::min(lo[a], x);
+                    hi[a] = std::max(hi[a], x);
+                }
+            }
+            E = std::max(E, std::max(std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]),
+                                     std::sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2])));
+        }
+        DevCluster &k = cl[c];
+        const double ctr[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
+        k.cx = (float)ctr[0];
+        k.cy = (float)ctr[1];
+        k.cz = (float)ctr[2];
+        double R = 0.0;
+        for (int j = 0; j < n; ++j) { /* radius about the rounded (float) centre */
+            const DevTri &r = ct[(size_t)c * kClusterSize + j];
+            const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
+            const double K[3] = {k.cx, k.cy, k.cz};
+            for (int w = 0; w < 3; ++w) {
+                double d2 = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    const double x = A[a] + (w == 1 ? B[a] : w == 2 ? C[a] : 0.0) - K[a];
+                    d2 += x * x;
+                }
+                R = std::max(R, std::sqrt(d2));
+            }
+        }
+        const double F = 4.0, edRatio = 8.0 * u * E * E * kClusterRhoMax / eps;
+        k.r = std::nextafter((float)(R * (1.0 + 1e-9)), INFINITY);
+        k.e = (float)E;
+        if (!finite || n == 0 || !(edRatio < 0.5) || !(k.r < 1e18f)) {
+            k.alpha = INFINITY; /* never culled */
+            k.beta = k.gammaE = 0.f;
+            continue;
+        }
+        const double kk = 1.0 / (1.0 - edRatio);
+        k.alpha = std::nextafter((float)(F * kk * 32.0 * u * E * E * E / eps), INFINITY);
+        k.beta = std::nextafter((float)(F * kk * 45.0 * u * E * E / eps), INFINITY);
+        k.gammaE = std::nextafter((float)(kClusterGamma * E), INFINITY);
+    }
+}
+
 extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount, int device,
                                 RtcDeviceScene **out)
 {
@@ -214,13 +345,27 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     std::vector<DevMat> dm;
     std::vector<DevSphere> ds;
     pack_scene(tris, triCount, spheres, sphereCount, dt, dm, ds);
+    std::vector<DevTri> ct;
+    std::vector<DevCluster> cl;
+    rtc_build_clusters(dt, triCount, ct, cl);
+    if (ct.empty())
+        ct.assign(1, DevTri{});
     RtcDeviceScene *s = new RtcDeviceScene();
     s->device = device;
     s->triCount = triCount;
     s->triPadded = (triCount + 7) / 8 * 8; /* whole pairs of batches; arrays hold 8 more records for prefetch */
     s->sphereCount = sphereCount;
     s->maskWords = (s->triPadded + 63) / 64;
+    s->clusterCount = (triCount + kClusterSize - 1) / kClusterSize;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->clTris, ct.size() * sizeof(DevTri));
+    if (e == hipSuccess)
+        e = hipMalloc(&s->clusters, cl.size() * sizeof(DevCluster));
+    if (e == hipSuccess)
+        e = hipMemcpy(s->clTris, ct.data(), ct.size() * sizeof(DevTri), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(s->clusters, cl.data(), cl.size() * sizeof(DevCluster), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
     if (e == hipSuccess)
@@ -263,6 +408,10 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
     (void)hipSetDevice(s->device);
     if (s->tris)
         (void)hipFree(s->tris);
+    if (s->clTris)
+        (void)hipFree(s->clTris);
+    if (s->clusters)
+        (void)hipFree(s->clusters);
     if (s->mats)
         (void)hipFree(s->mats);
     if (s->spheres)
@@ -301,6 +450,9 @@ struct RenderParams {
     const DevSphere *__restrict__ spheres;
     const DevPrimF *__restrict__ primF;
     const DevPrimX *__restrict__ primX;
+    const DevTri *__restrict__ clTris;         /* cluster order (rtc_build_clusters) */
+    const DevCluster *__restrict__ clusters;
+    int clusterCount, clusterCull;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
     int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter) */
@@ -485,6 +637,27 @@ __device__ __forceinline__ bool prim_pass(V3 dir, const DevPrimF &F)
     return (dt >= F.c) & (fminf(fminf(ut, vt), wt) >= F.negm);
 }
 
+/* The reference's arithmetic (raytracing.c:189-208) for a primary record the filter keeps. */
+__device__ __forceinline__ void primary_exact(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
+                                              Closest &c)
+{
+    const DevPrimX X = P.primX[t];
+    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
+        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
+        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
+        if (!(-kEps < det && det < kEps)) {
+            const float invDet = 1.f / det;
+            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
+            const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
+            const float dst = X.dac0 * invDet;
+            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                c.dst = dst;
+                c.idx = base + t;
+            }
+        }
+    }
+}
+
 /* One primary record (see closest_primary). */
 __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
                                              Closest &c)
@@ -572,7 +745,39 @@ __device__ __forceinline__ void closest_primary_listed(const RenderParams &P, V3
     }
 }
 
-/* General segments (any origin): rayTriangle (raytracing.c:186-214) with AB, AC precomputed. */
+/* General segments (any origin): rayTriangle (raytracing.c:186-214) with AB, AC precomputed.
+ * general_filter: the exact-safe rejection (backface, |det| < EPSILON, u out of range by the rcp estimate);
+ * general_exact: the reference's arithmetic for a record the filter keeps (recomputes the same values). */
+__device__ __forceinline__ bool general_filter(V3 pos, V3 dir, const DevTri &R)
+{
+    const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
+    const V3 AB{R.abx, R.aby, R.abz}, AC{R.acx, R.acy, R.acz};
+    const V3 h = cross(dir, AC);
+    const float det = dot(AB, h);
+    const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
+    const float uu = dot(s, h);
+    const float ua = uu * __builtin_amdgcn_rcpf(det);
+    const bool detOk = !(-kEps < det && det < kEps);
+    return (int)!(nd >= 0.f) & (int)detOk & (int)!(ua < -kTiny) & (int)!(ua > 1.000001f);
+}
+
+__device__ __forceinline__ void general_exact(V3 pos, V3 dir, const DevTri &R, int idx, Closest &c)
+{
+    const V3 AB{R.abx, R.aby, R.abz}, AC{R.acx, R.acy, R.acz};
+    const V3 h = cross(dir, AC);
+    const float det = dot(AB, h);
+    const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
+    const float invDet = 1.f / det;
+    const float u = dot(s, h) * invDet;
+    const V3 q = cross(s, AB);
+    const float v = dot(dir, q) * invDet;
+    const float dst = dot(AC, q) * invDet;
+    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+        c.dst = dst;
+        c.idx = idx;
+    }
+}
+
 __device__ __forceinline__ void general_test(V3 pos, V3 dir, const DevTri &R, int idx, Closest &c)
 {
     const float nd = dot(dir, V3{R.nx, R.ny, R.nz});
@@ -777,32 +982,35 @@ constexpr int kSegSlots = 256, kSegSlotStride = 16; /* u64 */
 static_assert(kSegSlots * kSegSlotStride == 256 * 16, "rtc_scene_upload allocates 256 x 16 u64");
 
 __device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned segCalls, unsigned segTraced,
-                                               unsigned long long segTests, int lane)
+                                               unsigned long long segTests, int lane, unsigned segClusters = 0)
 {
     if (!P.segments)
         return;
-    unsigned long long a = segCalls, b = segTraced, n = segTests;
+    unsigned long long a = segCalls, b = segTraced, n = segTests, k = segClusters;
     for (int off = 32; off > 0; off >>= 1) {
         a += __shfl_xor(a, off);
         b += __shfl_xor(b, off);
         n += __shfl_xor(n, off);
+        k += __shfl_xor(k, off);
     }
-    if (lane == 0 && (a | b | n)) {
+    if (lane == 0 && (a | b | n | k)) {
         const unsigned slot = (blockIdx.x * 7u + blockIdx.y * 131u + (threadIdx.x >> 6)) % kSegSlots;
         unsigned long long *c = P.segSlots + (size_t)slot * kSegSlotStride;
         atomicAdd(&c[0], a);
         atomicAdd(&c[1], b);
         atomicAdd(&c[2], n);
+        if (k)
+            atomicAdd(&c[3], k);
     }
 }
 
 __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(const unsigned long long *__restrict__ slots,
                                                                  unsigned long long *__restrict__ out)
 {
-    __shared__ unsigned long long part[3][kSegSlots / 64];
+    __shared__ unsigned long long part[4][kSegSlots / 64];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         unsigned long long v = slots[(size_t)t * kSegSlotStride + k];
         for (int off = 32; off > 0; off >>= 1)
             v += __shfl_xor(v, off);
@@ -810,7 +1018,7 @@ __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(const unsigned 
             part[k][w] = v;
     }
     __syncthreads();
-    if (t < 3) {
+    if (t < 4) {
         unsigned long long v = 0;
         for (int i = 0; i < kSegSlots / 64; ++i)
             v += part[t][i];
@@ -1048,7 +1256,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
  * Every value is produced by the same operations as in rtc_render_kernel, only on different lanes, so the
  * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
  * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
-constexpr int kCoop = 4;
+#ifndef RTC_COOP
+#define RTC_COOP 4
+#endif
+constexpr int kCoop = RTC_COOP;
+static_assert(kCoop == 4 || kCoop == 8, "the normals need 3 lanes and the shuffles a power of two");
+constexpr int kHeavyBlock = 64 * kCoop; /* one 8x8 tile per workgroup, kCoop lanes per pixel */
 #ifndef RTC_SKY_UNROLL
 #define RTC_SKY_UNROLL 2
 #endif
@@ -1088,22 +1301,81 @@ __global__ __launch_bounds__(1024) void rtc_order_heavy(const unsigned *__restri
 }
 
 
+/* True when the bounce ray (pos, dir) provably cannot hit any triangle of cluster K (see DevCluster): the
+ * half-line's distance to the ball centre exceeds r + eps.  rho = |dir|_1 >= |dir|; NaN never culls. */
+__device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, const DevCluster &K)
+{
+    const V3 w = sub(V3{K.cx, K.cy, K.cz}, pos);
+    const float S = fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + K.r; /* >= |pos - A| for every vertex A */
+    const float T = (K.r + rho * (K.alpha + K.beta * S) + kClusterGamma * S + K.gammaE) * 1.00001f;
+    const float T2 = T * T;
+    const float b = dot(w, dir);
+    const V3 x = cross(w, dir);
+    const float x2 = dot(x, x), w2 = dot(w, w);
+    /* b > 0: the closest point is interior, distance |w x dir| / |dir| >= sqrt(x2) / rho; else the origin */
+    return b > 0.f ? x2 > T2 * (rho * rho) : w2 > T2;
+}
+
 /* Cooperative calculateRayCollision for the kCoop lanes of one pixel (no spheres in the fused launch).
  * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
  * lane `sub` of a group reads record sub, sub+4, ... (four distinct records per wave instruction, each
  * broadcast to 16 lanes). */
 __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 dir, bool primarySeg,
-                                              const DevTri *__restrict__ sTri, const DevPrimF *__restrict__ sPrimF,
-                                              const int *__restrict__ sCand, int L, int sub)
+                                              const DevTri *__restrict__ sTri, const DevCluster *__restrict__ sCl,
+                                              const DevPrimF *__restrict__ sPrimF, const int *__restrict__ sCand,
+                                              int L, int sub, unsigned &testedTris)
 {
     Closest c{999999.f, -1};
+    testedTris = 0;
+    /* Two passes.  The lanes of a wave test unrelated (ray, record) pairs, so a branch inside the test runs
+     * for the whole wave whenever one lane needs it.  Pass 1 evaluates the exact-safe filter branch-free for
+     * all of this lane's records (at most 64: kLdsTris / kCoop) and keeps the survivors as bits; pass 2 runs
+     * the reference arithmetic for the survivors only, in index order.  Same operations as primary_test /
+     * general_test. */
+    unsigned long long surv = 0;
     if (primarySeg) {
-        for (int k = sub; k < L; k += kCoop)
-            primary_test(P, dir, sPrimF[k], sCand[k], 0, c);
+        for (int k = sub, b = 0; k < L; k += kCoop, ++b) {
+            const DevPrimF &F = sPrimF[k];
+            const bool keep = (int)!prim_backfacing(dir, F) & (int)prim_pass(dir, F);
+            surv |= (unsigned long long)keep << b;
+        }
+        while (surv) {
+            const int b = __builtin_ctzll(surv);
+            surv &= surv - 1;
+            const int k = sub + kCoop * b;
+            primary_exact(P, dir, sPrimF[k], sCand[k], 0, c);
+        }
     } else {
-#pragma unroll 2
-        for (int t = sub; t < P.triPadded; t += kCoop)
-            general_test(pos, dir, sTri[t], t, c);
+        /* bounce segment: the clusters a ray may hit (lane sub tests clusters sub, sub+kCoop, ...; OR over
+         * the group), then the records of those clusters, lane sub taking records sub, sub+kCoop, ... of each;
+         * survivor bit = cluster * kPer + j.  sTri holds the records in cluster order (pad0 = index). */
+        constexpr int kPer = kClusterSize / kCoop;
+        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+        const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+        unsigned cm = 0;
+        for (int k = sub; k < P.clusterCount; k += kCoop)
+            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, sCl[k])) << k;
+#pragma unroll
+        for (int k = 1; k < kCoop; k <<= 1)
+            cm |= (unsigned)__shfl_xor((int)cm, k);
+        /* triangles in the clusters kept (only the last cluster has zero records) */
+        testedTris = (unsigned)__popc(cm) * kClusterSize -
+                     ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+        unsigned m = cm;
+        while (m) {
+            const int k = __builtin_ctz(m);
+            m &= m - 1;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+                surv |= (unsigned long long)general_filter(pos, dir, sTri[k * kClusterSize + sub + kCoop * j])
+                        << (k * kPer + j);
+        }
+        while (surv) {
+            const int b = __builtin_ctzll(surv);
+            surv &= surv - 1;
+            const DevTri &R = sTri[(b / kPer) * kClusterSize + sub + kCoop * (b % kPer)];
+            general_exact(pos, dir, R, __float_as_int(R.pad0), c);
+        }
     }
 #pragma unroll
     for (int k = 1; k < kCoop; k <<= 1) {
@@ -1211,7 +1483,7 @@ __host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
 #ifndef RTC_HEAVY_WAVES
 #define RTC_HEAVY_WAVES 1
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
+__global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
     RenderParams P)
 {
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
@@ -1221,12 +1493,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
     int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
     int &sCount = sCand[P.triPadded];
     __shared__ int sItem;
+    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
     sPow.fill(threadIdx.x);
     sPow.attach(P.env);
-    for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
-        sTri[i] = P.tris[i];
+    for (int i = threadIdx.x; i < P.triPadded; i += kHeavyBlock) /* clusterCount * 8 == triPadded */
+        sTri[i] = P.clTris[i];
+    for (int i = threadIdx.x; i < P.clusterCount; i += kHeavyBlock)
+        sCl[i] = P.clusters[i];
     const int lane = threadIdx.x & 63;
-    unsigned segCalls = 0, segTraced = 0;
+    unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0;
     const int heavy = P.heavy[0]; /* rtc_order_heavy: number of heavy tiles; P.heavy[1]: next slot */
     for (;;) {
@@ -1238,6 +1513,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
             break;
         const int tile = P.order[slot];
         const int wave = threadIdx.x >> 6;
+#ifdef RTC_DIAG
+        const unsigned long long diagRt0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long diagC0 = __builtin_amdgcn_s_memtime();
+#endif
         const int tilesX = P.blocksX * 2;
         const int tx = tile % tilesX, ty = tile / tilesX;
         const int sub = lane & (kCoop - 1);
@@ -1262,7 +1541,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
         }
         __syncthreads();
         const unsigned L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
-        for (int k = threadIdx.x; k < (int)L; k += kBlock)
+        for (int k = threadIdx.x; k < (int)L; k += kHeavyBlock)
             sPrimF[k] = P.primF[sCand[k]];
         __syncthreads();
 
@@ -1273,7 +1552,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
         V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
         Closest primary{999999.f, -1};
         if (P.hoist && alive) {
-            primary = coop_trace(P, pos, dir, true, sTri, sPrimF, sCand, (int)L, sub);
+            unsigned nc;
+            primary = coop_trace(P, pos, dir, true, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
             segTraced++;
             segTests += L;
         }
@@ -1284,9 +1564,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
                 if (P.hoist && bounce == 0) {
                     c = primary;
                 } else {
-                    c = coop_trace(P, pos, dir, bounce == 0, sTri, sPrimF, sCand, (int)L, sub);
+                    unsigned nc = 0;
+                    c = coop_trace(P, pos, dir, bounce == 0, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
                     segTraced++;
-                    segTests += bounce == 0 ? L : (unsigned)P.triCount;
+                    segTests += bounce == 0 ? L : nc;
+                    segClusters += bounce == 0 ? 0u : (unsigned)P.clusterCount;
                 }
                 bool endSample;
                 if (c.idx >= 0) {
@@ -1340,12 +1622,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAV
             }
         }
         if (sub != 0) {
-            segCalls = segTraced = 0;
+            segCalls = segTraced = segClusters = 0;
             segTests = 0;
         }
         __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
+#ifdef RTC_DIAG
+        if (g_rtc_diag && threadIdx.x == 0) {
+            g_rtc_diag[4 * slot] = diagRt0;
+            g_rtc_diag[4 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+            g_rtc_diag[4 * slot + 2] = __builtin_amdgcn_s_memtime() - diagC0;
+            g_rtc_diag[4 * slot + 3] = ((unsigned long long)blockIdx.x << 32) | (unsigned)tile;
+        }
+#endif
     }
-    flush_counters(P, segCalls, segTraced, segTests, lane);
+    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
 }
 
 static EnvParams env_of(const Scene &s)
@@ -1387,6 +1677,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.segSlots = s->segSlots;
     P.triCount = s->triCount;
     P.triPadded = s->triPadded;
+    P.clTris = s->clTris;
+    P.clusters = s->clusters;
+    P.clusterCount = s->clusterCount;
+    P.clusterCull = !(d->flags & RTC_F_NO_CLUSTER_CULL);
     P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
     P.maskWords = s->maskWords;
     P.width = d->width;
@@ -1469,7 +1763,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
             hipLaunchKernelGGL(rtc_render_heavy, dim3((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers)),
-                               dim3(kBlock), rtc_heavy_lds_bytes(s->triPadded), st, P);
+                               dim3(kHeavyBlock), rtc_heavy_lds_bytes(s->triPadded), st, P);
             HIP_TRY(hipGetLastError());
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
@@ -1582,6 +1876,7 @@ extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *sphe
         stats->segments = seg[0];
         stats->samples = (unsigned long long)px * (unsigned long long)(d->spp > 0 ? d->spp : 0);
         stats->triTests = seg[2];
+        stats->clusterTests = seg[3];
         stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
@@ -1663,7 +1958,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             rc = rtc_fail(-(int)e, "event record: %s", hipGetErrorString(e));
     }
     double maxMs = 0;
-    unsigned long long segs = 0, tests = 0;
+    unsigned long long segs = 0, tests = 0, clusterTests = 0;
     std::vector<unsigned char> col;
     std::vector<float> acc;
     for (int g = 0; g < numDevices && !rc; ++g) {
@@ -1692,6 +1987,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             maxMs = ms;
         segs += sg[0];
         tests += sg[2];
+        clusterTests += sg[3];
         const size_t rowB = (size_t)d->width * 3;
         for (int k = 0; k < p.rows; ++k) {
             const int y = g + k * numDevices;
@@ -1708,6 +2004,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         stats->segments = segs;
         stats->samples = (unsigned long long)d->width * d->height * (unsigned long long)(d->spp > 0 ? d->spp : 0);
         stats->triTests = tests;
+        stats->clusterTests = clusterTests;
         stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
@@ -1779,6 +2076,46 @@ __global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, 
         V3 d = random_direction(s);
         dirs[i * draws + k] = vec3{d.x, d.y, d.z};
     }
+}
+
+/* Cluster culling soundness (DevCluster): every (ray, cluster) pair is culled or not by cluster_culled, and
+ * every triangle of the cluster is tested with the reference's rayTriangle arithmetic.  counts: [0] hits in
+ * culled clusters (must stay 0), [1] clusters culled, [2] cluster tests, [3] hits, [4] float bits of the
+ * largest (distance from the ball centre to the reported hit point) - r over all hits. */
+__global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl, int clusterCount, const Ray *rays,
+                                     size_t n, unsigned long long *counts)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const V3 pos = v3(rays[i].pos), dir = v3(rays[i].dir);
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    unsigned viol = 0, culled = 0, hits = 0;
+    float excess = 0.f;
+    for (int k = 0; k < clusterCount; ++k) {
+        const DevCluster K = cl[k];
+        const bool cut = rho <= kClusterRhoMax && cluster_culled(pos, dir, rho, K);
+        culled += cut;
+        for (int j = 0; j < kClusterSize; ++j) {
+            const DevTri R = clTris[k * kClusterSize + j];
+            if (__float_as_int(R.pad0) < 0)
+                continue;
+            float dst;
+            if (ray_triangle(pos, dir, V3{R.ax, R.ay, R.az}, V3{R.abx, R.aby, R.abz}, V3{R.acx, R.acy, R.acz},
+                             V3{R.nx, R.ny, R.nz}, dst)) {
+                hits++;
+                viol += cut;
+                const V3 h = add(pos, mul(dir, dst));
+                const V3 w = sub(h, V3{K.cx, K.cy, K.cz});
+                excess = fmaxf(excess, (float)__builtin_sqrt((double)dot(w, w)) - K.r);
+            }
+        }
+    }
+    atomicAdd(&counts[0], (unsigned long long)viol);
+    atomicAdd(&counts[1], (unsigned long long)culled);
+    atomicAdd(&counts[2], (unsigned long long)clusterCount);
+    atomicAdd(&counts[3], (unsigned long long)hits);
+    atomicMax(&counts[4], (unsigned long long)__float_as_uint(excess));
 }
 
 namespace {
@@ -1900,4 +2237,41 @@ extern "C" int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, 
     HIP_TRY(hipMemcpy(normal, dn, m * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(direction, dd, m * sizeof(vec3), hipMemcpyDeviceToHost));
     return 0;
+}
+
+extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
+                                       unsigned long long counts[5])
+{
+    if (!counts || triCount < 0 || (triCount > 0 && !tris) || (n > 0 && !rays))
+        return rtc_fail(RTC_EINVAL, "rtc_probe_cluster_bound: bad argument");
+    memset(counts, 0, 5 * sizeof(unsigned long long));
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0 || triCount == 0)
+        return 0;
+    RtcDeviceScene *s = nullptr;
+    if (int rc = rtc_scene_upload(tris, triCount, nullptr, 0, -1, &s))
+        return rc;
+    Scratch sc;
+    Ray *dr = nullptr;
+    unsigned long long *dc = nullptr;
+    int rc = 0;
+    hipError_t e = sc.alloc((void **)&dr, n * sizeof(Ray));
+    if (e == hipSuccess)
+        e = hipMemcpy(dr, rays, n * sizeof(Ray), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = sc.alloc((void **)&dc, 5 * sizeof(unsigned long long));
+    if (e == hipSuccess)
+        e = hipMemset(dc, 0, 5 * sizeof(unsigned long long));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->clusters,
+                           s->clusterCount, dr, n, dc);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipMemcpy(counts, dc, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e != hipSuccess)
+        rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
+    rtc_scene_release(s);
+    return rc;
 }

@@ -22,6 +22,7 @@ seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream()
 for name, t, cfg in [("empty", tris[:0], rt.RenderConfig(W, H, SPP, 10, True)),
                      ("faithful", tris, rt.RenderConfig(W, H, SPP, 10, True)),
+                     ("faithful_nocluster", tris, rt.RenderConfig(W, H, SPP, 10, True, cluster_cull=False)),
                      ("faithful_nocoop", tris, rt.RenderConfig(W, H, SPP, 10, True, coop=False)),
                      ("hoist", tris, rt.RenderConfig(W, H, SPP, 10, True, hoist=True))]:
     ds = rt.DeviceScene(t, None)
@@ -34,4 +35,6 @@ for name, t, cfg in [("empty", tris[:0], rt.RenderConfig(W, H, SPP, 10, True)),
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     ds.close()
-    print(json.dumps({"variant": name, "ms": [round(x, 3) for x in times]}), flush=True)
+    print(json.dumps({"variant": name, "ms": [round(x, 3) for x in times],
+                      "segments": [int(v) for v in seg.cpu()]}), flush=True)
+    seg.zero_()
