@@ -55,6 +55,9 @@ __device__ __forceinline__ float random_value(unsigned &s)
      * lies within r 2^-64 (< 2^-32) above r 2^-32, which cannot reach the next float rounding boundary but
      * does push an exact tie upward; r 2^-32 + r 2^-64 (one rounding) does the same.  Equal for all 2^32
      * values of r (checked exhaustively, tools/check_devmath.cpp). */
+#ifdef RTC_FAKE_RNG /* timing experiment only: not the reference's value */
+    return (float)r * 0x1p-32f;
+#endif
     const double d = (double)r * 0x1p-32;
     return (float)fma((double)r, 0x1p-64, d);
 }

@@ -454,6 +454,8 @@ struct RenderParams {
     const DevCluster *__restrict__ clusters;
     int clusterCount, clusterCull;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
+    const unsigned long long *__restrict__ pixMask;  /* per 8x8 tile: pixels with a primary candidate (bit i =
+                                                       pixel i, row-major); the others see only the sky */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
     int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter) */
     int blocksX; /* 16x16 blocks per row of the launch */
@@ -906,7 +908,8 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
  * unchanged, bit for bit.  The filter is the render kernel's own (prim_backfacing / prim_pass, same records,
  * same pixel_ray). */
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
-                                                       unsigned *__restrict__ weight, unsigned *__restrict__ tileW)
+                                                       unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
+                                                       unsigned long long *__restrict__ pixMask)
 {
     __shared__ unsigned wgWeight;
     if (threadIdx.x == 0)
@@ -939,8 +942,10 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
      * non-empty candidate list exactly when its weight is > 0 */
     const unsigned long long b = __ballot(anyCand);
-    if (lane == 0)
+    if (lane == 0) {
         tileW[wave_tile(bx, by)] = (unsigned)__popcll(b);
+        pixMask[wave_tile(bx, by)] = b;
+    }
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
     __syncthreads();
@@ -1035,6 +1040,30 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_diag), &dptr, sizeof dptr));
     return 0;
 }
+/* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
+ * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
+__device__ unsigned long long g_rtc_sect[8];
+__shared__ unsigned long long s_rtc_sect[16][8];
+#define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DSECT_END(v, k)                                                                                        \
+    do {                                                                                                       \
+        const unsigned long long dsectNow = __builtin_amdgcn_s_memtime();                                      \
+        if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))                           \
+            s_rtc_sect[threadIdx.x >> 6][k] += dsectNow - (v);                                                 \
+    } while (0)
+extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
+{
+    if (out8)
+        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 8 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[8] = {0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
+    }
+    return 0;
+}
+#else
+#define DSECT_BEGIN(v) (void)0
+#define DSECT_END(v, k) (void)0
 #endif
 
 #ifndef RTC_MIN_WAVES
@@ -1316,6 +1345,25 @@ __device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, const 
     return b > 0.f ? x2 > T2 * (rho * rho) : w2 > T2;
 }
 
+/* Position of the n-th (0-based) set bit of m; m must have more than n set bits. */
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n)
+{
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const unsigned long long low = m & ((1ull << w) - 1ull);
+        const int c = __popcll(low);
+        if (n >= c) {
+            n -= c;
+            pos += w;
+            m >>= w;
+        } else {
+            m = low;
+        }
+    }
+    return pos;
+}
+
 /* Cooperative calculateRayCollision for the kCoop lanes of one pixel (no spheres in the fused launch).
  * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
  * lane `sub` of a group reads record sub, sub+4, ... (four distinct records per wave instruction, each
@@ -1334,6 +1382,7 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
      * general_test. */
     unsigned long long surv = 0;
     if (primarySeg) {
+        DSECT_BEGIN(d0);
         for (int k = sub, b = 0; k < L; k += kCoop, ++b) {
             const DevPrimF &F = sPrimF[k];
             const bool keep = (int)!prim_backfacing(dir, F) & (int)prim_pass(dir, F);
@@ -1345,7 +1394,9 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
             const int k = sub + kCoop * b;
             primary_exact(P, dir, sPrimF[k], sCand[k], 0, c);
         }
+        DSECT_END(d0, 0);
     } else {
+        DSECT_BEGIN(d1);
         /* bounce segment: the clusters a ray may hit (lane sub tests clusters sub, sub+kCoop, ...; OR over
          * the group), then the records of those clusters, lane sub taking records sub, sub+kCoop, ... of each;
          * survivor bit = cluster * kPer + j.  sTri holds the records in cluster order (pad0 = index). */
@@ -1361,6 +1412,8 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
         /* triangles in the clusters kept (only the last cluster has zero records) */
         testedTris = (unsigned)__popc(cm) * kClusterSize -
                      ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+        DSECT_END(d1, 1);
+        DSECT_BEGIN(d2);
         unsigned m = cm;
         while (m) {
             const int k = __builtin_ctz(m);
@@ -1370,13 +1423,17 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
                 surv |= (unsigned long long)general_filter(pos, dir, sTri[k * kClusterSize + sub + kCoop * j])
                         << (k * kPer + j);
         }
+        DSECT_END(d2, 2);
+        DSECT_BEGIN(d3);
         while (surv) {
             const int b = __builtin_ctzll(surv);
             surv &= surv - 1;
             const DevTri &R = sTri[(b / kPer) * kClusterSize + sub + kCoop * (b % kPer)];
             general_exact(pos, dir, R, __float_as_int(R.pad0), c);
         }
+        DSECT_END(d3, 3);
     }
+    DSECT_BEGIN(d4);
 #pragma unroll
     for (int k = 1; k < kCoop; k <<= 1) {
         const float od = __shfl_xor(c.dst, k);
@@ -1386,6 +1443,7 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
             c.idx = oi;
         }
     }
+    DSECT_END(d4, 4);
     return c;
 }
 
@@ -1404,9 +1462,13 @@ __device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int gr
         }
     }
     /* RandomValueNormalDistrubtion (moremath.c:97-102) */
+#ifdef RTC_FAKE_BM /* timing experiment only: not the reference's value */
+    const float n = sqrtf(-2.f * __logf(uRho)) * __cosf(6.2831853f * uTheta);
+#else
     const float theta = (float)(2 * 3.14159265 * (double)uTheta);
     const float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)uRho));
     const float n = (float)((double)rho * rtcmath::cos((double)theta));
+#endif
     const float nx = __shfl(n, groupBase), ny = __shfl(n, groupBase + 1), nz = __shfl(n, groupBase + 2);
     return normalized(V3{nx, ny, nz});
 }
@@ -1441,9 +1503,14 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
     unsigned segCalls = 0, segTraced = 0;
     {
         const int bx = blockIdx.x, by = blockIdx.y;
-        if (tileW[wave_tile(bx, by)] > 0)
+        /* pixels without a primary candidate: their primary ray misses every triangle (the filter is exact-safe),
+         * so every sample is one segment ending in the sky, in heavy tiles too (rtc_render_heavy skips them) */
+        const int t = wave_tile(bx, by);
+        const unsigned long long geo = tileW[t] > 0 ? P.pixMask[t] : 0ull;
+        if (geo == ~0ull)
             return;
-        const PixelRay px = pixel_ray(P, bx, by);
+        PixelRay px = pixel_ray(P, bx, by);
+        px.valid = px.valid && !((geo >> lane) & 1ull);
         V3 acc{0.f, 0.f, 0.f};
         if (px.valid && P.spp > 0 && P.maxBounce > 0) {
             /* see the skyTile path of rtc_render_kernel */
@@ -1475,9 +1542,13 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
  * tiles see geometry.  Dynamic LDS: the scene's records, the tile's candidate records and indices
  * (rtc_heavy_lds_bytes). */
 constexpr int kHeavyWorkers = 2048;
+#ifndef RTC_COOP_PRIMARY_LIST
+#define RTC_COOP_PRIMARY_LIST 1
+#endif
+constexpr bool kPrimaryList = RTC_COOP_PRIMARY_LIST != 0;
 __host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
 {
-    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(int)) + 16;
+    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(int)) + 16;
 }
 
 #ifndef RTC_HEAVY_WAVES
@@ -1490,7 +1561,8 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ PowTablesLds sPow;
     DevTri *sTri = (DevTri *)sDyn;
     DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
-    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
+    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
+    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
     int &sCount = sCand[P.triPadded];
     __shared__ int sItem;
     __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
@@ -1500,6 +1572,18 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         sTri[i] = P.clTris[i];
     for (int i = threadIdx.x; i < P.clusterCount; i += kHeavyBlock)
         sCl[i] = P.clusters[i];
+    for (int i = threadIdx.x; i < P.triPadded; i += kHeavyBlock) { /* shading records by reference index */
+        DevMat m = P.mats[i];
+        const DevTri &t = P.tris[i];
+        m.pad0 = t.nx;
+        m.pad1 = t.ny;
+        m.pad2 = t.nz;
+        sShade[i] = m;
+    }
+#ifdef RTC_DIAG
+    if ((threadIdx.x & 63) < 8)
+        s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+#endif
     const int lane = threadIdx.x & 63;
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0;
@@ -1521,11 +1605,19 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const int tx = tile % tilesX, ty = tile / tilesX;
         const int sub = lane & (kCoop - 1);
         const int groupBase = lane & ~(kCoop - 1);
-        const int pi = wave * (64 / kCoop) + lane / kCoop; /* pixel of the 8x8 tile, row-major */
+        /* the tile's pixels with primary candidates, packed: wave w takes the (16w + lane/kCoop)-th of them
+         * (row-major); rtc_render_sky renders the others, and waves past the last one only keep the barriers */
+        const unsigned long long geo = P.pixMask[tile];
+        const int slotPx = wave * (64 / kCoop) + lane / kCoop;
+        const bool valid = slotPx < __popcll(geo);
+        const int pi = nth_set_bit(geo, valid ? slotPx : 0); /* pixel of the 8x8 tile, row-major */
         const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
-        const bool valid = x < P.width && r < P.rows;
         const int y = P.rowStart + r * P.rowStride;
         const V3 pdir = primary_dir(P, x, y);
+        /* Primary segments visit the tile's candidate list (RTC_COOP_PRIMARY_LIST=0: the cluster path like
+         * bounce segments -- one code path for the wave, but ~3x the triangle tests: measured slower). */
+        unsigned L = 0;
+        if (kPrimaryList) {
         /* LDS: the tile's primary candidates (index order) and their records */
         if (wave == 0) {
             const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
@@ -1540,10 +1632,11 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 sCount = base;
         }
         __syncthreads();
-        const unsigned L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
+        L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
         for (int k = threadIdx.x; k < (int)L; k += kHeavyBlock)
             sPrimF[k] = P.primF[sCand[k]];
         __syncthreads();
+        }
 
         unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
         V3 acc{0.f, 0.f, 0.f};
@@ -1552,12 +1645,14 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
         Closest primary{999999.f, -1};
         if (P.hoist && alive) {
-            unsigned nc;
-            primary = coop_trace(P, pos, dir, true, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+            unsigned nc = 0;
+            primary = coop_trace(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
             segTraced++;
-            segTests += L;
+            segTests += kPrimaryList ? L : nc;
+            segClusters += kPrimaryList ? 0u : (unsigned)P.clusterCount;
         }
         while (__any(alive)) {
+            DSECT_BEGIN(d7);
             if (alive) {
                 Closest c;
                 segCalls++;
@@ -1565,18 +1660,19 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     c = primary;
                 } else {
                     unsigned nc = 0;
-                    c = coop_trace(P, pos, dir, bounce == 0, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+                    const bool listed = kPrimaryList && bounce == 0;
+                    c = coop_trace(P, pos, dir, listed, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
                     segTraced++;
-                    segTests += bounce == 0 ? L : nc;
-                    segClusters += bounce == 0 ? 0u : (unsigned)P.clusterCount;
+                    segTests += listed ? L : nc;
+                    segClusters += listed ? 0u : (unsigned)P.clusterCount;
                 }
                 bool endSample;
                 if (c.idx >= 0) {
+                    DSECT_BEGIN(d5);
                     /* calcColor hit branch, raytracing.c:272-287 */
                     const V3 hitPoint = add(pos, mul(dir, c.dst));
-                    const DevTri T = P.tris[c.idx];
-                    const DevMat M = P.mats[c.idx];
-                    const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
+                    const DevMat M = sShade[c.idx]; /* material, pad0..2 = the stored normal */
+                    const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
                     const V3 diffuseDir = normalized(add(normal, random_direction_coop(rng, sub, groupBase)));
                     const V3 specularDir = reflect(dir, normal);
                     dir = lerp(diffuseDir, specularDir, M.smoothness);
@@ -1591,9 +1687,12 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         bounce++;
                         endSample = bounce >= P.maxBounce;
                     }
+                    DSECT_END(d5, 5);
                 } else {
+                    DSECT_BEGIN(d6);
                     light = add(light, mulv(environment_coop(dir, P.env, sub, groupBase), rayColor));
                     endSample = true;
+                    DSECT_END(d6, 6);
                 }
                 if (endSample) {
                     acc = add(acc, mul(light, P.invSpp)); /* main.c:99 */
@@ -1609,6 +1708,7 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     }
                 }
             }
+            DSECT_END(d7, 7);
         }
         if (valid && sub == 0) {
             const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
@@ -1635,6 +1735,10 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
 #endif
     }
+#ifdef RTC_DIAG
+    if (lane < 8)
+        atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
+#endif
     flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
 }
 
@@ -1713,7 +1817,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     if (cull) {
-        const size_t need = maskBytes + (blocks + tiles + tiles + blocks + 4) * sizeof(int);
+        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int);
         if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (ms->scratch)
@@ -1739,11 +1843,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                            s->primF, s->primX, s->triPadded + 8, P.origin);
     if (cull) {
         unsigned long long *mask = (unsigned long long *)s->scratch;
-        unsigned *weight = (unsigned *)(s->scratch + maskBytes);
+        unsigned long long *pixMask = mask + tiles * (size_t)s->maskWords;
+        unsigned *weight = (unsigned *)(pixMask + tiles);
         unsigned *tileW = weight + blocks;
         int *order = (int *)(tileW + tiles);
-        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW);
+        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW, pixMask);
         P.tileMask = mask;
+        P.pixMask = pixMask;
         if (fused) {
             /* sky tiles on the side stream, concurrently with the heavy tiles on `st`; `st` then waits for both */
             int *heavy = order + tiles + blocks;

@@ -26,15 +26,24 @@ rt.check(rt.lib().rtc_diag_set_buffer(C.c_void_p(buf.data_ptr())), "diag")
 out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
 ds = rt.DeviceScene(tris, None)
 stream = torch.cuda.current_stream()
+rt.lib().rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
+sect = np.zeros(8, np.uint64)
+NAMES = ["primary_trace", "cluster_tests", "gen_filter", "gen_exact", "lane_reduce", "hit_shading", "sky_miss",
+         "loop_total"]
 for hoist in (False, True):
     cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist)
     for rep in range(2):
         buf.zero_()
+        rt.check(rt.lib().rtc_diag_sections(None, 1), "sections")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, None, stream.cuda_stream)
         e1.record(stream)
         torch.cuda.synchronize()
+    rt.check(rt.lib().rtc_diag_sections(sect.ctypes.data_as(C.c_void_p), 0), "sections")
+    tot = float(sect[7])
+    print(json.dumps({"hoist": hoist, "section_share_of_loop": {n: round(float(v) / tot, 3) for n, v in zip(NAMES, sect)},
+                      "loop_cycles_per_wave": round(tot / (len(np.unique(buf.view(tiles, 4)[:, 3].cpu().numpy() >> 32)) * 4), 0)}))
     d = buf.view(tiles, 4).cpu().numpy()
     m = d[:, 1] > 0
     d = d[m]
