@@ -211,6 +211,12 @@ class DeviceScene:
                                           C.c_void_p(segments_ptr) if segments_ptr else None,
                                           C.c_void_p(stream) if stream else None), "rtc_render_rows_async")
 
+    def kernel_times(self):
+        """(heavy-tile kernel ms, sky kernel ms) of the last split launch (None if it was not one)."""
+        out = (C.c_float * 2)()
+        check(lib().rtc_scene_kernel_times(self._h, out), "rtc_scene_kernel_times")
+        return None if out[0] < 0 else (float(out[0]), float(out[1]))
+
     def close(self):
         if self._h:
             lib().rtc_scene_release(self._h)

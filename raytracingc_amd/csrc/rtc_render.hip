@@ -170,6 +170,9 @@ struct RtcDeviceScene {
     /* the split launch runs the sky kernel on `side`, concurrently with the heavy-tile kernel */
     hipStream_t side;
     hipEvent_t evFork, evJoin;
+    /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
+    hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
+    bool timed; /* the last launch was a split launch that recorded them */
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -391,6 +394,9 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
+    for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
+        if (e == hipSuccess)
+            e = hipEventCreate(ev);
     if (e != hipSuccess) {
         rtc_scene_release(s);
         return rtc_fail(-(int)e, "scene upload failed: %s", hipGetErrorString(e));
@@ -428,6 +434,9 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
         (void)hipEventDestroy(s->evJoin);
+    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1})
+        if (ev)
+            (void)hipEventDestroy(ev);
     if (s->side)
         (void)hipStreamDestroy(s->side);
     if (cur >= 0)
@@ -1864,17 +1873,24 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evFork, st));
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
             }
+            RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
+            HIP_TRY(hipEventRecord(s->evSky0, skyStream));
             hipLaunchKernelGGL(rtc_render_sky, grid, dim3(kBlock), 0, skyStream, P, (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(s->evSky1, skyStream));
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
+            HIP_TRY(hipEventRecord(s->evHeavy0, st));
             hipLaunchKernelGGL(rtc_render_heavy, dim3((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers)),
                                dim3(kHeavyBlock), rtc_heavy_lds_bytes(s->triPadded), st, P);
             HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(s->evHeavy1, st));
+            ms->timed = true;
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
             return finish();
         }
+        const_cast<RtcDeviceScene *>(s)->timed = false;
         hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
         P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
     }
@@ -2380,4 +2396,18 @@ extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const
         rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
     rtc_scene_release(s);
     return rc;
+}
+
+extern "C" int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2])
+{
+    if (!s || !out)
+        return rtc_fail(RTC_EINVAL, "rtc_scene_kernel_times: null argument");
+    out[0] = out[1] = -1.f;
+    if (!s->timed)
+        return 0;
+    HIP_TRY(hipEventSynchronize(s->evHeavy1));
+    HIP_TRY(hipEventSynchronize(s->evSky1));
+    HIP_TRY(hipEventElapsedTime(&out[0], s->evHeavy0, s->evHeavy1));
+    HIP_TRY(hipEventElapsedTime(&out[1], s->evSky0, s->evSky1));
+    return 0;
 }

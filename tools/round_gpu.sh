@@ -30,6 +30,7 @@ if [ "$what" = all ] || [ "$what" = prof ]; then
   step rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-hoisted || exit $?
   step pmc_fetch 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o p --output-format csv -- python3 "$R/tools/one_render.py" faithful 2 || exit $?
   step pmc_write 90 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o p --output-format csv -- python3 "$R/tools/one_render.py" faithful 2 || exit $?
+  cd "$R" && python3 tools/pmc_traffic.py "$OUT" > "$OUT/pmc_traffic.log" 2>&1; cd /tmp
   step pmc_sq 90 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o p --output-format csv -- python3 "$R/tools/one_render.py" faithful 2 || exit $?
 fi
 echo done
