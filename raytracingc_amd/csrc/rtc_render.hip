@@ -916,6 +916,108 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
  * of the tile, so the reference's rayTriangle rejects it for every primary ray there: the closest hit is
  * unchanged, bit for bit.  The filter is the render kernel's own (prim_backfacing / prim_pass, same records,
  * same pixel_ray). */
+/* Tile prefilter.  The per-pixel filter values nd, dt, ut, vt, wt are (FMA) dot products of the pixel's f32
+ * direction d with per-triangle vectors g.  Over an 8x8 tile, d = v / |v| with v = ex dx + ey dy + ez fov
+ * affine in the pixel's (dx, dy), which lie in the rectangle spanned by the tile's extreme pixels (dx, dy
+ * are monotone in x, y).  So g.v takes its extremes at the rectangle's corners, |v| lies in [vmin, vmax]
+ * (vmax: |v| is convex, a corner; vmin: v.ez/|ez| is affine, its smallest corner value, when positive), and
+ * g.d (exact direction) lies in [LB, UB] with UB = Amax / vmin or Amax / vmax by the sign of the corner
+ * maximum Amax (LB likewise).  The computed value differs from g.d(exact) by at most
+ *   |g|_1 (eDir + 3.01 u),  eDir = 16 u S / vmin + 4 u  (u = 2^-24, S = max|dx| + max|dy| + |fov|)
+ * (f32 v: 3 roundings per component, <= 3 u S each; normalisation <= 2 u; the FMA dot <= 3 u |g|_1; the
+ * constants carry ~1.5x).  A triangle is left out of the tile when one filter condition fails for every
+ * point of that range -- then it fails for every pixel, exactly as the per-pixel filter would decide.
+ * Computed in double per (tile, triangle); a tile whose bounds are not finite or whose vmin <= 0 is never
+ * pruned. */
+struct TileCone {
+    double c[4][3];
+    double vmin, vmax, eDir;
+    bool ok;
+};
+
+__device__ TileCone tile_cone(const RenderParams &P, int tx, int ty)
+{
+    TileCone K;
+    const int x0 = tx * 8, x1 = min(tx * 8 + 7, P.width - 1);
+    const int r0 = ty * 8, r1 = min(ty * 8 + 7, P.rows - 1);
+    const int y0 = P.rowStart + r0 * P.rowStride, y1 = P.rowStart + r1 * P.rowStride;
+    /* the same f32 expressions as primary_dir */
+    const float dxs[2] = {(float)(x0 - P.width / 2) / (float)(P.height / 2),
+                          (float)(x1 - P.width / 2) / (float)(P.height / 2)};
+    const float dys[2] = {(float)(y0 - P.height / 2) / (float)(P.height / 2),
+                          (float)(y1 - P.height / 2) / (float)(P.height / 2)};
+    const double ezl = sqrt((double)P.ez.x * P.ez.x + (double)P.ez.y * P.ez.y + (double)P.ez.z * P.ez.z);
+    double vmin = 1e300, vmax = 0.0;
+    bool finite = ezl > 0.0 && ezl < 1e300;
+    for (int k = 0; k < 4; ++k) {
+        const double dx = dxs[k & 1], dy = dys[k >> 1];
+        const double v[3] = {(double)P.ex.x * dx + (double)P.ey.x * dy + (double)P.ez.x * P.fov,
+                             (double)P.ex.y * dx + (double)P.ey.y * dy + (double)P.ez.y * P.fov,
+                             (double)P.ex.z * dx + (double)P.ey.z * dy + (double)P.ez.z * P.fov};
+        for (int i = 0; i < 3; ++i) {
+            K.c[k][i] = v[i];
+            finite = finite && (v[i] - v[i] == 0.0);
+        }
+        vmax = fmax(vmax, sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]));
+        vmin = fmin(vmin, (v[0] * P.ez.x + v[1] * P.ez.y + v[2] * P.ez.z) / ezl);
+    }
+    const double u = 5.9604644775390625e-08;
+    const double S = fmax(fabs((double)dxs[0]), fabs((double)dxs[1])) + fmax(fabs((double)dys[0]), fabs((double)dys[1])) +
+                     fabs((double)P.fov);
+    K.vmin = vmin * (1.0 - 1e-12);
+    K.vmax = vmax * (1.0 + 1e-12);
+    K.eDir = 16.0 * u * S / K.vmin + 4.0 * u;
+    /* basis components <= 1 (normalized f32 vectors) is assumed by the error bound */
+    const bool unitBasis = fabs(P.ex.x) <= 1.0001f && fabs(P.ex.y) <= 1.0001f && fabs(P.ex.z) <= 1.0001f &&
+                           fabs(P.ey.x) <= 1.0001f && fabs(P.ey.y) <= 1.0001f && fabs(P.ey.z) <= 1.0001f &&
+                           fabs(P.ez.x) <= 1.0001f && fabs(P.ez.y) <= 1.0001f && fabs(P.ez.z) <= 1.0001f;
+    K.ok = finite && unitBasis && K.vmin > 1e-6 && K.eDir < 1e-3 && S - S == 0.0;
+    return K;
+}
+
+/* [LB, UB] of g.v/|v| over the tile (see TileCone) */
+__device__ __forceinline__ void cone_range(const TileCone &K, double gx, double gy, double gz, double &lb, double &ub)
+{
+    double mx = -1e300, mn = 1e300;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double a = gx * K.c[k][0] + gy * K.c[k][1] + gz * K.c[k][2];
+        mx = fmax(mx, a);
+        mn = fmin(mn, a);
+    }
+    ub = mx >= 0.0 ? mx / K.vmin : mx / K.vmax;
+    lb = mn >= 0.0 ? mn / K.vmax : mn / K.vmin;
+}
+
+/* true: no pixel of the tile can pass prim_backfacing / prim_pass for F */
+__device__ bool tile_prunes(const TileCone &K, const DevPrimF &F)
+{
+    const double u = 5.9604644775390625e-08;
+    const double e = K.eDir + 3.01 * u;
+    auto n1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
+    double lb, ub;
+    /* every pixel back-facing: nd > mnd */
+    cone_range(K, F.nx, F.ny, F.nz, lb, ub);
+    if (lb - n1(F.nx, F.ny, F.nz) * e > (double)F.mnd)
+        return true;
+    const double nd = n1(F.gdx, F.gdy, F.gdz), nu = n1(F.gux, F.guy, F.guz), nv = n1(F.q0x, F.q0y, F.q0z);
+    cone_range(K, F.gdx, F.gdy, F.gdz, lb, ub);
+    if (ub + nd * e < (double)F.c)
+        return true;
+    cone_range(K, F.gux, F.guy, F.guz, lb, ub);
+    if (ub + nu * e < (double)F.negm)
+        return true;
+    cone_range(K, F.q0x, F.q0y, F.q0z, lb, ub);
+    if (ub + nv * e < (double)F.negm)
+        return true;
+    /* wt = (dt - ut) - vt: the three slacks plus two f32 subtractions */
+    cone_range(K, (double)F.gdx - F.gux - F.q0x, (double)F.gdy - F.guy - F.q0y, (double)F.gdz - F.guz - F.q0z, lb,
+               ub);
+    if (ub + (nd + nu + nv) * (e + 2.01 * u * 1.0001) < (double)F.negm)
+        return true;
+    return false;
+}
+
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
                                                        unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
                                                        unsigned long long *__restrict__ pixMask)
@@ -927,23 +1029,27 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     const int bx = blockIdx.x, by = blockIdx.y;
     const PixelRay px = pixel_ray(P, bx, by);
     const int lane = threadIdx.x & 63;
-    unsigned long long *out = mask + (size_t)wave_tile(bx, by) * P.maskWords;
+    const int tile = wave_tile(bx, by);
+    unsigned long long *out = mask + (size_t)tile * P.maskWords;
     bool anyCand = false;
+#ifndef RTC_TILE_PREFILTER
+#define RTC_TILE_PREFILTER 1
+#endif
+    const TileCone K = tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2));
     for (int w = 0; w < P.maskWords; ++w) {
+        /* lane l: may triangle 64w + l pass for some pixel of the tile? */
+        const int ti = w * 64 + lane;
+        const bool maybe = ti < P.triPadded && (!RTC_TILE_PREFILTER || !K.ok || !tile_prunes(K, P.primF[ti]));
+        unsigned long long todo = __ballot(maybe);
         unsigned long long bits = 0;
-        const int n = min(64, P.triPadded - w * 64); /* a multiple of 8 */
-        for (int k0 = 0; k0 < n; k0 += 4) {
-            DevPrimF F[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                F[j] = P.primF[w * 64 + k0 + j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool keep = (int)px.valid & (int)!prim_backfacing(px.dir, F[j]) & (int)prim_pass(px.dir, F[j]);
-                anyCand |= keep;
-                if (__ballot(keep))
-                    bits |= 1ull << (k0 + j);
-            }
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const DevPrimF F = P.primF[w * 64 + j];
+            const bool keep = (int)px.valid & (int)!prim_backfacing(px.dir, F) & (int)prim_pass(px.dir, F);
+            anyCand |= keep;
+            if (__ballot(keep))
+                bits |= 1ull << j;
         }
         if (lane == 0)
             out[w] = bits;
@@ -952,8 +1058,8 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
      * non-empty candidate list exactly when its weight is > 0 */
     const unsigned long long b = __ballot(anyCand);
     if (lane == 0) {
-        tileW[wave_tile(bx, by)] = (unsigned)__popcll(b);
-        pixMask[wave_tile(bx, by)] = b;
+        tileW[tile] = (unsigned)__popcll(b);
+        pixMask[tile] = b;
     }
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
