@@ -1628,11 +1628,18 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
         px.valid = px.valid && !((geo >> lane) & 1ull);
         V3 acc{0.f, 0.f, 0.f};
         if (px.valid && P.spp > 0 && P.maxBounce > 0) {
-            /* see the skyTile path of rtc_render_kernel */
-#pragma unroll RTC_SKY_UNROLL
-            for (int s = 0; s < P.spp; ++s) {
+            /* see the skyTile path of rtc_render_kernel.  Hoisted mode evaluates the primary ray's miss once
+             * (a function of the pixel, like its closest hit); faithful mode evaluates it every sample. */
+            if (P.hoist) {
                 const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
-                acc = add(acc, mul(l, P.invSpp));
+                for (int s = 0; s < P.spp; ++s)
+                    acc = add(acc, mul(l, P.invSpp));
+            } else {
+#pragma unroll RTC_SKY_UNROLL
+                for (int s = 0; s < P.spp; ++s) {
+                    const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
+                    acc = add(acc, mul(l, P.invSpp));
+                }
             }
             segCalls = (unsigned)P.spp;
             segTraced = P.hoist ? 1u : (unsigned)P.spp;

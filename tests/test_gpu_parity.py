@@ -170,6 +170,31 @@ def test_tile_cull_many_triangles(gpu_available):
     assert over == 0 and s1["segments"] == oseg
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_tile_cull_random_cameras(seed, gpu_available):
+    """The tile prefilter (TileCone: a bound of the primary filter over each 8x8 tile's direction cone) and the
+    cluster culling under random cameras, fields of view and frame shapes, rows partitions included: the
+    split launch == brute force (RTC_F_NO_TILE_CULL, every primary segment tests every triangle), bit for
+    bit, with the same segment counts."""
+    rng = np.random.default_rng(seed)
+    name = ["ultracomplex", "complex", "fsuzane"][seed % 3]
+    tris, tonly = load_tris(name)
+    origin = tuple(float(v) for v in rng.uniform(-9, 9, 3))
+    look = tuple(float(v) for v in rng.uniform(-1.5, 1.5, 3) + np.array([0, 2.5, 0]))
+    fov = float(rng.choice([0.35, 1.0, 1.7, 3.0]))
+    cam = rt.camera_basis(origin, look, fov)
+    scene = rt.default_scene()
+    w, h = int(rng.integers(24, 150)), int(rng.integers(9, 120))
+    stride = int(rng.choice([1, 1, 3]))
+    base = rt.RenderConfig(w, h, 3, 10, bool(tonly), row_start=int(rng.integers(0, stride)), row_stride=stride)
+    c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**base.__dict__, "tile_cull": False}),
+                           want_accum=True)
+    c1, a1, s1 = rt.render(tris, None, scene, cam, base, want_accum=True)
+    assert np.array_equal(_bits(a0), _bits(a1)) and np.array_equal(c0, c1)
+    assert s0["segments"] == s1["segments"]
+    print(f"{name} {w}x{h} fov={fov} origin={origin}: tests {s0['tri_tests']} -> {s1['tri_tests']}")
+
+
 def test_tile_cull_full_frame(gpu_available):
     """The BASELINE frame (ultracomplex 1920x1080, 16 spp here): culled == brute force bit for bit, and the
     culled run evaluates far fewer ray-triangle tests."""
