@@ -18,8 +18,9 @@ LIB      := $(LIBDIR)/librtc.so
 CLI      := $(LIBDIR)/rtc
 ORACLE   := oracle/liboracle.so
 REFBIN   := oracle/_ref/rtc_ref
+PROBE    := $(LIBDIR)/exact_probe
 
-all: $(LIB) $(CLI) $(ORACLE) ref
+all: $(LIB) $(CLI) $(ORACLE) $(PROBE) ref
 
 $(BUILD):
 	mkdir -p $(BUILD) $(LIBDIR) oracle/_ref
@@ -42,6 +43,12 @@ $(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/scene_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 diag: $(DIAGLIB)
+
+# exhaustive GPU check of the exact f32 shortcuts (tests/test_gpu_exact.py)
+$(PROBE): tools/exact_probe.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h | $(BUILD)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -ffp-contract=off -std=c++17 $< -o $@
+
+probe: $(PROBE)
 
 $(BUILD)/rtc_main.o: $(CSRC)/rtc_main.c include/rtc.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@

@@ -63,6 +63,9 @@ typedef struct RtcRenderDesc {
                                     with 4 cooperating lanes per pixel (A/B timing; the frame is identical) */
 #define RTC_F_NO_CLUSTER_CULL 0x20 /* bounce rays of the cooperative path test every triangle instead of only
                                       the clusters their half-line may reach (A/B timing; identical frame) */
+#define RTC_F_COOP4         0x40 /* force 4 cooperating lanes per pixel (default: 8 for launches of at most
+                                    700k pixels, else 4; identical frame) */
+#define RTC_F_COOP8         0x80 /* force 8 cooperating lanes per pixel (identical frame) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render kernel(s), HIP events */

@@ -29,11 +29,32 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)                                 
 {
     return V3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
+/* Correctly rounded f32 sqrt.  The reference's sqrt of a float in double, rounded to float, is the same
+ * value (double rounding is innocuous for sqrt: 53 >= 2*24+2); llvm.sqrt.f32 is correctly rounded under
+ * HIP's default -fhip-fp32-correctly-rounded-divide-sqrt.  Checked for all 2^32 inputs
+ * (tools/exact_probe.hip, tests/test_gpu_exact.py). */
+__device__ __forceinline__ float sqrt_cr(float x) { return __builtin_sqrtf(x); }
+
+/* Correctly rounded 1/x, == the IEEE f32 divide 1.f / x (and so == (float)(1./x)).  For |x| in
+ * [2^-125, 2^125]: v_rcp_f32 (<= 1 ulp) and two FMA Newton steps (the residual 1 - x r is exact in an FMA when
+ * r is within an ulp; the second step leaves an error far below the distance of 1/x from any rounding
+ * midpoint); other x take the divide.  Checked for all 2^32 inputs (tools/exact_probe.hip). */
+__device__ __forceinline__ float rcp_cr(float x)
+{
+    const float ax = __builtin_fabsf(x);
+    if (ax >= 0x1p-125f && ax <= 0x1p125f) {
+        float r = __builtin_amdgcn_rcpf(x);
+        r = __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    }
+    return 1.f / x;
+}
+
 /* length (moremath.c:7-10): sqrt of the f32 sum in double, rounded to float (== correctly rounded sqrtf) */
-__device__ __forceinline__ float length(V3 v) { return (float)__builtin_sqrt((double)(v.x * v.x + v.y * v.y + v.z * v.z)); }
+__device__ __forceinline__ float length(V3 v) { return sqrt_cr(v.x * v.x + v.y * v.y + v.z * v.z); }
 __device__ __forceinline__ V3 normalized(V3 v) /* :12-17 */
 {
-    float invLen = 1.f / length(v);
+    float invLen = rcp_cr(length(v)); /* (float)(1./length(v)) */
     return V3{v.x * invLen, v.y * invLen, v.z * invLen};
 }
 __device__ __forceinline__ float clamp01(float x) { return x < 0.f ? 0.f : (x > 1.f ? 1.f : x); } /* :38-41 */
@@ -61,6 +82,29 @@ __device__ __forceinline__ float random_value(unsigned &s)
     const double d = (double)r * 0x1p-32;
     return (float)fma((double)r, 0x1p-64, d);
 }
+/* The LCG step of RandomValue is affine mod 2^32, so k steps are one: s_k = A_k s + C_k with A_k = a^k and
+ * C_k = c (a^(k-1) + ... + 1).  rng_jump_value(s, k) is the value of the k-th draw from state s (k >= 1),
+ * i.e. what k calls of random_value would return last; it does not advance s. */
+struct RngJump {
+    unsigned a, c;
+};
+constexpr RngJump rng_jump(int k)
+{
+    unsigned A = 1u, C = 0u;
+    for (int i = 0; i < k; ++i) {
+        C = C * 747796405u + 2891336453u;
+        A = A * 747796405u;
+    }
+    return RngJump{A, C};
+}
+__device__ __forceinline__ float rng_value_of_state(unsigned s)
+{
+    unsigned r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;
+    r = (r >> 22) ^ r;
+    const double d = (double)r * 0x1p-32;
+    return (float)fma((double)r, 0x1p-64, d);
+}
+
 /* RandomValueNormalDistrubtion (moremath.c:97-102): Box-Muller cos branch in double */
 __device__ __forceinline__ float random_normal(unsigned &s)
 {
@@ -137,7 +181,7 @@ __device__ __forceinline__ bool ray_triangle(V3 pos, V3 dir, V3 A, V3 AB, V3 AC,
     float det = dot(AB, h);
     if (-kEps < det && det < kEps)
         return false;
-    float invDet = 1.f / det;
+    float invDet = rcp_cr(det); /* IEEE 1.f / det */
     V3 s = sub(pos, A);
     float u = dot(s, h) * invDet;
     if (u < 0.f || u > 1.f)

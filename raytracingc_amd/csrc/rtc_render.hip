@@ -657,7 +657,7 @@ __device__ __forceinline__ void primary_exact(const RenderParams &P, V3 dir, con
         const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
         const float det = dot(V3{X.abx, X.aby, X.abz}, h);
         if (!(-kEps < det && det < kEps)) {
-            const float invDet = 1.f / det;
+            const float invDet = rcp_cr(det); /* IEEE 1.f / det */
             const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
             const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
             const float dst = X.dac0 * invDet;
@@ -681,7 +681,7 @@ __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, cons
                 const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
                 const float det = dot(V3{X.abx, X.aby, X.abz}, h);
                 if (!(-kEps < det && det < kEps)) {
-                    const float invDet = 1.f / det;
+                    const float invDet = rcp_cr(det); /* IEEE 1.f / det */
                     const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
                     const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
                     const float dst = X.dac0 * invDet;
@@ -778,7 +778,7 @@ __device__ __forceinline__ void general_exact(V3 pos, V3 dir, const DevTri &R, i
     const V3 h = cross(dir, AC);
     const float det = dot(AB, h);
     const V3 s = sub(pos, V3{R.ax, R.ay, R.az});
-    const float invDet = 1.f / det;
+    const float invDet = rcp_cr(det); /* IEEE 1.f / det */
     const float u = dot(s, h) * invDet;
     const V3 q = cross(s, AB);
     const float v = dot(dir, q) * invDet;
@@ -802,7 +802,7 @@ __device__ __forceinline__ void general_test(V3 pos, V3 dir, const DevTri &R, in
         const float ua = uu * r;
         const bool detOk = !(-kEps < det && det < kEps);
         if (detOk & !(ua < -kTiny) & !(ua > 1.000001f)) {
-            const float invDet = 1.f / det;
+            const float invDet = rcp_cr(det); /* IEEE 1.f / det */
             const float u = uu * invDet;
             const V3 q = cross(s, AB);
             const float v = dot(dir, q) * invDet;
@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
                 const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
                 endSample = p < random_value(rng);
                 if (!endSample) {
-                    rayColor = mul(rayColor, 1.f / p);
+                    rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
                     bounce++;
                     endSample = bounce >= P.maxBounce;
                 }
@@ -1400,12 +1400,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
  * Every value is produced by the same operations as in rtc_render_kernel, only on different lanes, so the
  * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
  * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
-#ifndef RTC_COOP
-#define RTC_COOP 4
+/* KC (the lanes per pixel, a template parameter of the heavy path) is 4 for full frames and 8 for small
+ * launches (a rank's share of a multi-GPU frame, see rtc_render_rows_async): 8 lanes split the trace
+ * further and evaluate the six Box-Muller transcendentals on six lanes, shortening each pixel's chain. */
+#ifndef RTC_COOP8_MAX_PIXELS
+#define RTC_COOP8_MAX_PIXELS 700000
 #endif
-constexpr int kCoop = RTC_COOP;
-static_assert(kCoop == 4 || kCoop == 8, "the normals need 3 lanes and the shuffles a power of two");
-constexpr int kHeavyBlock = 64 * kCoop; /* one 8x8 tile per workgroup, kCoop lanes per pixel */
 #ifndef RTC_SKY_UNROLL
 #define RTC_SKY_UNROLL 2
 #endif
@@ -1483,6 +1483,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, int n)
  * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
  * lane `sub` of a group reads record sub, sub+4, ... (four distinct records per wave instruction, each
  * broadcast to 16 lanes). */
+template <int KC>
 __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 dir, bool primarySeg,
                                               const DevTri *__restrict__ sTri, const DevCluster *__restrict__ sCl,
                                               const DevPrimF *__restrict__ sPrimF, const int *__restrict__ sCand,
@@ -1492,13 +1493,13 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
     testedTris = 0;
     /* Two passes.  The lanes of a wave test unrelated (ray, record) pairs, so a branch inside the test runs
      * for the whole wave whenever one lane needs it.  Pass 1 evaluates the exact-safe filter branch-free for
-     * all of this lane's records (at most 64: kLdsTris / kCoop) and keeps the survivors as bits; pass 2 runs
+     * all of this lane's records (at most 64: kLdsTris / KC) and keeps the survivors as bits; pass 2 runs
      * the reference arithmetic for the survivors only, in index order.  Same operations as primary_test /
      * general_test. */
     unsigned long long surv = 0;
     if (primarySeg) {
         DSECT_BEGIN(d0);
-        for (int k = sub, b = 0; k < L; k += kCoop, ++b) {
+        for (int k = sub, b = 0; k < L; k += KC, ++b) {
             const DevPrimF &F = sPrimF[k];
             const bool keep = (int)!prim_backfacing(dir, F) & (int)prim_pass(dir, F);
             surv |= (unsigned long long)keep << b;
@@ -1506,23 +1507,23 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
         while (surv) {
             const int b = __builtin_ctzll(surv);
             surv &= surv - 1;
-            const int k = sub + kCoop * b;
+            const int k = sub + KC * b;
             primary_exact(P, dir, sPrimF[k], sCand[k], 0, c);
         }
         DSECT_END(d0, 0);
     } else {
         DSECT_BEGIN(d1);
-        /* bounce segment: the clusters a ray may hit (lane sub tests clusters sub, sub+kCoop, ...; OR over
-         * the group), then the records of those clusters, lane sub taking records sub, sub+kCoop, ... of each;
+        /* bounce segment: the clusters a ray may hit (lane sub tests clusters sub, sub+KC, ...; OR over
+         * the group), then the records of those clusters, lane sub taking records sub, sub+KC, ... of each;
          * survivor bit = cluster * kPer + j.  sTri holds the records in cluster order (pad0 = index). */
-        constexpr int kPer = kClusterSize / kCoop;
+        constexpr int kPer = kClusterSize / KC;
         const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
         const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
         unsigned cm = 0;
-        for (int k = sub; k < P.clusterCount; k += kCoop)
+        for (int k = sub; k < P.clusterCount; k += KC)
             cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, sCl[k])) << k;
 #pragma unroll
-        for (int k = 1; k < kCoop; k <<= 1)
+        for (int k = 1; k < KC; k <<= 1)
             cm |= (unsigned)__shfl_xor((int)cm, k);
         /* triangles in the clusters kept (only the last cluster has zero records) */
         testedTris = (unsigned)__popc(cm) * kClusterSize -
@@ -1535,7 +1536,7 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
             m &= m - 1;
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
-                surv |= (unsigned long long)general_filter(pos, dir, sTri[k * kClusterSize + sub + kCoop * j])
+                surv |= (unsigned long long)general_filter(pos, dir, sTri[k * kClusterSize + sub + KC * j])
                         << (k * kPer + j);
         }
         DSECT_END(d2, 2);
@@ -1543,14 +1544,14 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
         while (surv) {
             const int b = __builtin_ctzll(surv);
             surv &= surv - 1;
-            const DevTri &R = sTri[(b / kPer) * kClusterSize + sub + kCoop * (b % kPer)];
+            const DevTri &R = sTri[(b / kPer) * kClusterSize + sub + KC * (b % kPer)];
             general_exact(pos, dir, R, __float_as_int(R.pad0), c);
         }
         DSECT_END(d3, 3);
     }
     DSECT_BEGIN(d4);
 #pragma unroll
-    for (int k = 1; k < kCoop; k <<= 1) {
+    for (int k = 1; k < KC; k <<= 1) {
         const float od = __shfl_xor(c.dst, k);
         const int oi = __shfl_xor(c.idx, k);
         if (od < c.dst || (od == c.dst && (unsigned)oi < (unsigned)c.idx)) {
@@ -1562,28 +1563,48 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
     return c;
 }
 
-/* RandomDiretion (moremath.c:104-108) with the three normals on three lanes of the pixel's group */
+/* RandomDiretion (moremath.c:104-108) with the three normals on lanes of the pixel's group.
+ * KC = 4: lane k < 3 evaluates normal k (its two draws 2k+1, 2k+2, jumped to directly, see RngJump; the
+ * log, sqrt and cos of RandomValueNormalDistrubtion, moremath.c:97-102).  KC >= 8: lane k < 3 evaluates
+ * rho_k = (float)sqrt(-2 log u), lane 3 + k cos(theta_k), and lane k forms (float)(rho_k * cos_k): one
+ * transcendental per lane instead of two in sequence.  Every lane advances its state by the six draws. */
+template <int KC>
 __device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int groupBase)
 {
-    const int mine = sub < 3 ? sub : 0;
-    float uTheta = 0.f, uRho = 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float a = random_value(s);
-        const float b = random_value(s);
-        if (k == mine) {
-            uTheta = a;
-            uRho = b;
-        }
-    }
-    /* RandomValueNormalDistrubtion (moremath.c:97-102) */
+    constexpr RngJump j1 = rng_jump(1), j2 = rng_jump(2), j3 = rng_jump(3), j4 = rng_jump(4), j5 = rng_jump(5),
+                      j6 = rng_jump(6);
+    float n;
+    if constexpr (KC == 4) {
+        const int mine = sub < 3 ? sub : 0;
+        const unsigned aA = mine == 0 ? j1.a : (mine == 1 ? j3.a : j5.a);
+        const unsigned aC = mine == 0 ? j1.c : (mine == 1 ? j3.c : j5.c);
+        const unsigned bA = mine == 0 ? j2.a : (mine == 1 ? j4.a : j6.a);
+        const unsigned bC = mine == 0 ? j2.c : (mine == 1 ? j4.c : j6.c);
+        const float uTheta = rng_value_of_state(s * aA + aC);
+        const float uRho = rng_value_of_state(s * bA + bC);
 #ifdef RTC_FAKE_BM /* timing experiment only: not the reference's value */
-    const float n = sqrtf(-2.f * __logf(uRho)) * __cosf(6.2831853f * uTheta);
+        n = sqrtf(-2.f * __logf(uRho)) * __cosf(6.2831853f * uTheta);
 #else
-    const float theta = (float)(2 * 3.14159265 * (double)uTheta);
-    const float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)uRho));
-    const float n = (float)((double)rho * rtcmath::cos((double)theta));
+        const float theta = (float)(2 * 3.14159265 * (double)uTheta);
+        const float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)uRho));
+        n = (float)((double)rho * rtcmath::cos((double)theta));
 #endif
+    } else {
+        /* lane k < 3: draw 2k+2 (rho); lane 3 <= k < 6: draw 2(k-3)+1 (theta) */
+        const int k = sub < 3 ? sub : (sub < 6 ? sub - 3 : 0);
+        const bool isRho = sub < 3;
+        const unsigned dA = isRho ? (k == 0 ? j2.a : (k == 1 ? j4.a : j6.a)) : (k == 0 ? j1.a : (k == 1 ? j3.a : j5.a));
+        const unsigned dC = isRho ? (k == 0 ? j2.c : (k == 1 ? j4.c : j6.c)) : (k == 0 ? j1.c : (k == 1 ? j3.c : j5.c));
+        const float u = rng_value_of_state(s * dA + dC);
+        double t;
+        if (isRho)
+            t = (double)(float)__builtin_sqrt(-2 * rtcmath::log((double)u));
+        else
+            t = rtcmath::cos((double)(float)(2 * 3.14159265 * (double)u));
+        const double c = __shfl(t, groupBase + 3 + (sub < 3 ? sub : 0));
+        n = (float)(t * c); /* valid on lanes 0..2: rho_k * cos_k */
+    }
+    s = s * j6.a + j6.c;
     const float nx = __shfl(n, groupBase), ny = __shfl(n, groupBase + 1), nz = __shfl(n, groupBase + 2);
     return normalized(V3{nx, ny, nz});
 }
@@ -1676,7 +1697,8 @@ __host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
 #ifndef RTC_HEAVY_WAVES
 #define RTC_HEAVY_WAVES 1
 #endif
-__global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
+template <int KC>
+__global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
     RenderParams P)
 {
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
@@ -1690,11 +1712,11 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
     sPow.fill(threadIdx.x);
     sPow.attach(P.env);
-    for (int i = threadIdx.x; i < P.triPadded; i += kHeavyBlock) /* clusterCount * 8 == triPadded */
+    for (int i = threadIdx.x; i < P.triPadded; i += (64 * KC)) /* clusterCount * 8 == triPadded */
         sTri[i] = P.clTris[i];
-    for (int i = threadIdx.x; i < P.clusterCount; i += kHeavyBlock)
+    for (int i = threadIdx.x; i < P.clusterCount; i += (64 * KC))
         sCl[i] = P.clusters[i];
-    for (int i = threadIdx.x; i < P.triPadded; i += kHeavyBlock) { /* shading records by reference index */
+    for (int i = threadIdx.x; i < P.triPadded; i += (64 * KC)) { /* shading records by reference index */
         DevMat m = P.mats[i];
         const DevTri &t = P.tris[i];
         m.pad0 = t.nx;
@@ -1710,9 +1732,16 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0;
     const int heavy = P.heavy[0]; /* rtc_order_heavy: number of heavy tiles; P.heavy[1]: next slot */
+#ifdef RTC_DIAG
+    __shared__ unsigned sIters;
+#endif
     for (;;) {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             sItem = atomicAdd(&P.heavy[1], 1);
+#ifdef RTC_DIAG
+            sIters = 0;
+#endif
+        }
         __syncthreads();
         const int slot = __builtin_amdgcn_readfirstlane(sItem);
         if (slot >= heavy)
@@ -1721,16 +1750,16 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const int wave = threadIdx.x >> 6;
 #ifdef RTC_DIAG
         const unsigned long long diagRt0 = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long diagC0 = __builtin_amdgcn_s_memtime();
+        unsigned diagIters = 0;
 #endif
         const int tilesX = P.blocksX * 2;
         const int tx = tile % tilesX, ty = tile / tilesX;
-        const int sub = lane & (kCoop - 1);
-        const int groupBase = lane & ~(kCoop - 1);
-        /* the tile's pixels with primary candidates, packed: wave w takes the (16w + lane/kCoop)-th of them
+        const int sub = lane & (KC - 1);
+        const int groupBase = lane & ~(KC - 1);
+        /* the tile's pixels with primary candidates, packed: wave w takes the (16w + lane/KC)-th of them
          * (row-major); rtc_render_sky renders the others, and waves past the last one only keep the barriers */
         const unsigned long long geo = P.pixMask[tile];
-        const int slotPx = wave * (64 / kCoop) + lane / kCoop;
+        const int slotPx = wave * (64 / KC) + lane / KC;
         const bool valid = slotPx < __popcll(geo);
         const int pi = nth_set_bit(geo, valid ? slotPx : 0); /* pixel of the 8x8 tile, row-major */
         const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
@@ -1755,7 +1784,7 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
         __syncthreads();
         L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
-        for (int k = threadIdx.x; k < (int)L; k += kHeavyBlock)
+        for (int k = threadIdx.x; k < (int)L; k += (64 * KC))
             sPrimF[k] = P.primF[sCand[k]];
         __syncthreads();
         }
@@ -1768,12 +1797,15 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
         Closest primary{999999.f, -1};
         if (P.hoist && alive) {
             unsigned nc = 0;
-            primary = coop_trace(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+            primary = coop_trace<KC>(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
             segTraced++;
             segTests += kPrimaryList ? L : nc;
             segClusters += kPrimaryList ? 0u : (unsigned)P.clusterCount;
         }
         while (__any(alive)) {
+#ifdef RTC_DIAG
+            diagIters++;
+#endif
             DSECT_BEGIN(d7);
             if (alive) {
                 Closest c;
@@ -1783,7 +1815,7 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 } else {
                     unsigned nc = 0;
                     const bool listed = kPrimaryList && bounce == 0;
-                    c = coop_trace(P, pos, dir, listed, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+                    c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
                     segTraced++;
                     segTests += listed ? L : nc;
                     segClusters += listed ? 0u : (unsigned)P.clusterCount;
@@ -1795,7 +1827,7 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     const V3 hitPoint = add(pos, mul(dir, c.dst));
                     const DevMat M = sShade[c.idx]; /* material, pad0..2 = the stored normal */
                     const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
-                    const V3 diffuseDir = normalized(add(normal, random_direction_coop(rng, sub, groupBase)));
+                    const V3 diffuseDir = normalized(add(normal, random_direction_coop<KC>(rng, sub, groupBase)));
                     const V3 specularDir = reflect(dir, normal);
                     dir = lerp(diffuseDir, specularDir, M.smoothness);
                     pos = hitPoint;
@@ -1805,7 +1837,7 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
                     endSample = p < random_value(rng);
                     if (!endSample) {
-                        rayColor = mul(rayColor, 1.f / p);
+                        rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
                         bounce++;
                         endSample = bounce >= P.maxBounce;
                     }
@@ -1847,12 +1879,16 @@ __global__ __launch_bounds__(kHeavyBlock) __attribute__((amdgpu_waves_per_eu(RTC
             segCalls = segTraced = segClusters = 0;
             segTests = 0;
         }
+#ifdef RTC_DIAG
+        if (lane == 0)
+            atomicMax(&sIters, diagIters);
+#endif
         __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
 #ifdef RTC_DIAG
         if (g_rtc_diag && threadIdx.x == 0) {
             g_rtc_diag[4 * slot] = diagRt0;
             g_rtc_diag[4 * slot + 1] = __builtin_amdgcn_s_memrealtime();
-            g_rtc_diag[4 * slot + 2] = __builtin_amdgcn_s_memtime() - diagC0;
+            g_rtc_diag[4 * slot + 2] = sIters;
             g_rtc_diag[4 * slot + 3] = ((unsigned long long)blockIdx.x << 32) | (unsigned)tile;
         }
 #endif
@@ -1994,8 +2030,14 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
             HIP_TRY(hipEventRecord(s->evHeavy0, st));
-            hipLaunchKernelGGL(rtc_render_heavy, dim3((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers)),
-                               dim3(kHeavyBlock), rtc_heavy_lds_bytes(s->triPadded), st, P);
+            const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
+            /* small launches: 8 lanes per pixel (shorter chains; see KC) */
+            const bool eight = (d->flags & RTC_F_COOP8) ||
+                               (!(d->flags & RTC_F_COOP4) && (size_t)d->width * (size_t)rows <= (size_t)RTC_COOP8_MAX_PIXELS);
+            if (eight)
+                hipLaunchKernelGGL(rtc_render_heavy<8>, workers, dim3(64 * 8), rtc_heavy_lds_bytes(s->triPadded), st, P);
+            else
+                hipLaunchKernelGGL(rtc_render_heavy<4>, workers, dim3(64 * 4), rtc_heavy_lds_bytes(s->triPadded), st, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(s->evHeavy1, st));
             ms->timed = true;

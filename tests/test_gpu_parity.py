@@ -143,6 +143,12 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
     # (primary segments always visit only the candidates in the cooperative path, even when other pixels of
     # the wave are on later bounces: fewer tests)
     assert s1["segments"] == s2["segments"] and s1["tri_tests"] <= s2["tri_tests"]
+    # 4 and 8 cooperating lanes per pixel (RTC_F_COOP4 / RTC_F_COOP8): same bits, same counters
+    for lanes in (4, 8):
+        c3, a3, s3 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "coop_lanes": lanes}),
+                               want_accum=True)
+        assert np.array_equal(_bits(a1), _bits(a3)) and np.array_equal(c1, c3)
+        assert s1["segments"] == s3["segments"] and s1["tri_tests"] == s3["tri_tests"]
     print(f"{name} hoist={hoist}: tests {s0['tri_tests']} -> {s1['tri_tests']}")
 
 

@@ -30,8 +30,9 @@ rt.lib().rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
 sect = np.zeros(8, np.uint64)
 NAMES = ["primary_trace", "cluster_tests", "gen_filter", "gen_exact", "lane_reduce", "hit_shading", "sky_miss",
          "loop_total"]
+STRIDE = int(os.environ.get("DIAG_STRIDE", "1"))
 for hoist in (False, True):
-    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist)
+    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, row_stride=STRIDE)
     for rep in range(2):
         buf.zero_()
         rt.check(rt.lib().rtc_diag_sections(None, 1), "sections")
@@ -60,6 +61,8 @@ for hoist in (False, True):
                       "start_us_p50": q(start, 50), "start_us_max": round(float(start.max()), 1),
                       "end_us_max": round(float(end.max()), 1),
                       "tiles_started_after_200us": int((start > 200).sum()),
-                      "cycles_per_tile_p50": q(d[:, 2], 50)}), flush=True)
+                      "iters_p50": q(d[:, 2], 50), "iters_max": int(d[:, 2].max()),
+                      "us_per_iter_p50": q(dur / np.maximum(d[:, 2], 1), 50),
+                      "longest_tile_iters": int(d[np.argmax(dur), 2])}), flush=True)
     np.save(os.path.join(REPO, "gpurun_out", f"heavy_diag_hoist{int(hoist)}.npy"), d)
 ds.close()
