@@ -97,6 +97,25 @@ constexpr RngJump rng_jump(int k)
     }
     return RngJump{A, C};
 }
+/* jump by any k draws: compose the power-of-two jumps of k's set bits */
+constexpr RngJump rng_compose(RngJump x, RngJump y) { return RngJump{x.a * y.a, x.c * y.a + y.c}; } /* x then y */
+struct RngPow2Table {
+    RngJump j[32];
+    constexpr RngPow2Table() : j{}
+    {
+        j[0] = rng_jump(1);
+        for (int b = 1; b < 32; ++b)
+            j[b] = rng_compose(j[b - 1], j[b - 1]);
+    }
+};
+__device__ __forceinline__ unsigned rng_advance(unsigned s, unsigned k)
+{
+    constexpr RngPow2Table T;
+    for (int b = 0; b < 32 && (k >> b) != 0u; ++b)
+        if ((k >> b) & 1u)
+            s = s * T.j[b].a + T.j[b].c;
+    return s;
+}
 __device__ __forceinline__ float rng_value_of_state(unsigned s)
 {
     unsigned r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;

@@ -466,7 +466,9 @@ struct RenderParams {
     const unsigned long long *__restrict__ pixMask;  /* per 8x8 tile: pixels with a primary candidate (bit i =
                                                        pixel i, row-major); the others see only the sky */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
-    int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter) */
+    int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter),
+                                      [2] geometry pixels in pixList */
+    const int *__restrict__ pixList; /* geometry pixels of the heavy tiles, heaviest tile first: tile*64 + bit */
     int blocksX; /* 16x16 blocks per row of the launch */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
@@ -783,7 +785,10 @@ __device__ __forceinline__ void general_exact(V3 pos, V3 dir, const DevTri &R, i
     const V3 q = cross(s, AB);
     const float v = dot(dir, q) * invDet;
     const float dst = dot(AC, q) * invDet;
-    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+    /* records may be visited out of index order (clusters): equal distances keep the lowest index, as the
+     * reference's strict `<` over ascending indices does (raytracing.c:231) */
+    if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) &&
+        (dst < c.dst || (dst == c.dst && (unsigned)idx < (unsigned)c.idx))) {
         c.dst = dst;
         c.idx = idx;
     }
@@ -1157,7 +1162,7 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 }
 /* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
-__device__ unsigned long long g_rtc_sect[8];
+__device__ unsigned long long g_rtc_sect[16]; /* [8..] sample statistics (rtc_render_heavy) */
 __shared__ unsigned long long s_rtc_sect[16][8];
 #define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define DSECT_END(v, k)                                                                                        \
@@ -1169,9 +1174,9 @@ __shared__ unsigned long long s_rtc_sect[16][8];
 extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
 {
     if (out8)
-        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 8 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 16 * sizeof(unsigned long long)));
     if (reset) {
-        unsigned long long z[8] = {0};
+        unsigned long long z[16] = {0};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
     }
     return 0;
@@ -1750,7 +1755,7 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
         const int wave = threadIdx.x >> 6;
 #ifdef RTC_DIAG
         const unsigned long long diagRt0 = __builtin_amdgcn_s_memrealtime();
-        unsigned diagIters = 0;
+        unsigned diagIters = 0, diagHits = 0, diagSamples = 0, diagNon7 = 0, diagZero = 0;
 #endif
         const int tilesX = P.blocksX * 2;
         const int tx = tile % tilesX, ty = tile / tilesX;
@@ -1826,6 +1831,9 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
                     /* calcColor hit branch, raytracing.c:272-287 */
                     const V3 hitPoint = add(pos, mul(dir, c.dst));
                     const DevMat M = sShade[c.idx]; /* material, pad0..2 = the stored normal */
+#ifdef RTC_DIAG
+                    diagHits++;
+#endif
                     const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
                     const V3 diffuseDir = normalized(add(normal, random_direction_coop<KC>(rng, sub, groupBase)));
                     const V3 specularDir = reflect(dir, normal);
@@ -1851,6 +1859,12 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
                 if (endSample) {
                     acc = add(acc, mul(light, P.invSpp)); /* main.c:99 */
                     sample++;
+#ifdef RTC_DIAG
+                    diagSamples++;
+                    diagNon7 += diagHits != 1;
+                    diagZero += diagHits == 0;
+                    diagHits = 0;
+#endif
                     if (sample >= P.spp) {
                         alive = false;
                     } else {
@@ -1882,6 +1896,13 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
 #ifdef RTC_DIAG
         if (lane == 0)
             atomicMax(&sIters, diagIters);
+        if (valid && sub == 0) { /* per pixel: samples, samples with != 1 hit (!= 7 draws), with 0 hits */
+            atomicAdd(&g_rtc_sect[8], (unsigned long long)diagSamples);
+            atomicAdd(&g_rtc_sect[9], (unsigned long long)diagNon7);
+            atomicAdd(&g_rtc_sect[10], (unsigned long long)diagZero);
+            atomicAdd(&g_rtc_sect[11], 1ull);
+            atomicMax(&g_rtc_sect[12], (unsigned long long)diagNon7);
+        }
 #endif
         __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
 #ifdef RTC_DIAG
@@ -1898,6 +1919,289 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
 #endif
     flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
+}
+
+
+/* ---- sample-parallel speculative kernel (rtc_render_spec) ------------------------------------------------
+ * A pixel's samples are a chain only through the RNG state (main.c:95-100): sample s starts where sample s-1
+ * left it, after 7 draws per hit (6 for RandomDiretion, 1 for the roulette, raytracing.c:276-285).  In the
+ * tiles with geometry ~99.4 % of samples take exactly as many draws as the sample before them (the primary
+ * ray is the same for every sample, and bounce rays rarely hit again), so the next 64 samples can start
+ * together: lane i takes the state of the last validated sample advanced by D*i draws (rng_advance), where D
+ * is the draw count of the last validated sample.  After the round every lane up to and including the first
+ * one whose own draw count differs from D is correct (its start state assumed only earlier lanes); those
+ * samples are accumulated in sample order (main.c:99) and the next round starts after the last of them.
+ * Same operations as the reference on every value kept; the frame is bit-identical.  One wave per geometry
+ * pixel (rtc_pixel_list), 64 samples per round: a pixel's chain is a few segments long, not 2 x spp. */
+__global__ __launch_bounds__(1024) void rtc_pixel_list(const int *__restrict__ order, const unsigned long long *__restrict__ pixMask,
+                                                       int *__restrict__ heavy, int *__restrict__ list)
+{
+    __shared__ int part[1024];
+    __shared__ int running;
+    const int H = heavy[0];
+    if (threadIdx.x == 0)
+        running = 0;
+    __syncthreads();
+    for (int j0 = 0; j0 < H; j0 += 1024) {
+        const int j = j0 + threadIdx.x;
+        const int tile = j < H ? order[j] : -1;
+        const unsigned long long m = tile >= 0 ? pixMask[tile] : 0ull;
+        const int n = __popcll(m);
+        part[threadIdx.x] = n;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) { /* inclusive scan */
+            const int v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
+            __syncthreads();
+            part[threadIdx.x] += v;
+            __syncthreads();
+        }
+        int w = running + part[threadIdx.x] - n;
+        for (unsigned long long b = m; b; b &= b - 1)
+            list[w++] = tile * 64 + __builtin_ctzll(b);
+        __syncthreads();
+        if (threadIdx.x == 1023)
+            running += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        heavy[2] = running;
+        heavy[3] = 0;
+    }
+}
+
+/* Primary segments of the speculative kernel: the tile's candidates (bit-set in global memory, scalar
+ * loads) over the primary records staged in the workgroup's LDS, ascending index order (strict `<` ties). */
+__device__ __forceinline__ void primary_listed_lds(V3 dir, Closest &c, const unsigned long long *__restrict__ mask,
+                                                   int maskWords, const DevPrimF *__restrict__ sF,
+                                                   const DevPrimX *__restrict__ sX)
+{
+    for (int w = 0; w < maskWords; ++w) {
+        unsigned long long m = mask[w];
+        while (m) {
+            const int t = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const DevPrimF &F = sF[t];
+            if (!prim_backfacing(dir, F) && prim_pass(dir, F)) {
+                /* the reference's arithmetic (raytracing.c:189-208), as primary_test */
+                const DevPrimX &X = sX[t];
+                if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
+                    const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
+                    const float det = dot(V3{X.abx, X.aby, X.abz}, h);
+                    if (!(-kEps < det && det < kEps)) {
+                        const float invDet = rcp_cr(det); /* IEEE 1.f / det */
+                        const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
+                        const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
+                        const float dst = X.dac0 * invDet;
+                        if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                            c.dst = dst;
+                            c.idx = t;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* calculateRayCollision for one lane's bounce ray over the clusters it may reach (see DevCluster) */
+__device__ __forceinline__ Closest trace_clusters(const RenderParams &P, V3 pos, V3 dir, const DevTri *__restrict__ sTri,
+                                                  const DevCluster *__restrict__ sCl, unsigned &tests)
+{
+    Closest c{999999.f, -1};
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+    for (int k = 0; k < P.clusterCount; ++k) {
+        if (rhoOk && cluster_culled(pos, dir, rho, sCl[k]))
+            continue;
+        tests += (unsigned)min(kClusterSize, P.triCount - k * kClusterSize);
+        unsigned surv = 0;
+#pragma unroll
+        for (int j = 0; j < kClusterSize; ++j)
+            surv |= (unsigned)general_filter(pos, dir, sTri[k * kClusterSize + j]) << j;
+        while (surv) {
+            const int j = __builtin_ctz(surv);
+            surv &= surv - 1;
+            const DevTri &R = sTri[k * kClusterSize + j];
+            general_exact(pos, dir, R, __float_as_int(R.pad0), c);
+        }
+    }
+    return c;
+}
+
+constexpr int kSpecBlock = 256;
+__global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
+{
+    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
+    __shared__ PowTablesLds sPow;
+    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
+    DevTri *sTri = (DevTri *)sDyn;
+    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
+    DevPrimF *sPF = (DevPrimF *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevMat)));
+    DevPrimX *sPX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF)));
+    sPow.fill(threadIdx.x);
+    sPow.attach(P.env);
+    for (int i = threadIdx.x; i < P.triPadded; i += kSpecBlock) { /* clusterCount * 8 == triPadded */
+        sTri[i] = P.clTris[i];
+        sPF[i] = P.primF[i];
+        sPX[i] = P.primX[i];
+    }
+    for (int i = threadIdx.x; i < P.clusterCount; i += kSpecBlock)
+        sCl[i] = P.clusters[i];
+    for (int i = threadIdx.x; i < P.triPadded; i += kSpecBlock) { /* shading records by reference index */
+        DevMat m = P.mats[i];
+        const DevTri &t = P.tris[i];
+        m.pad0 = t.nx;
+        m.pad1 = t.ny;
+        m.pad2 = t.nz;
+        sShade[i] = m;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int items = P.heavy[2];
+    unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segClusters = 0;
+    for (;;) {
+        /* one pixel per fetch, heaviest tiles first (P.heavy[3]: the next item) */
+        int it = 0;
+        if (lane == 0)
+            it = atomicAdd(&P.heavy[3], 1);
+        it = __builtin_amdgcn_readfirstlane(it);
+        if (it >= items)
+            break;
+        const int code = __builtin_amdgcn_readfirstlane(P.pixList[it]);
+        const int tile = code >> 6, bit = code & 63;
+        const int tilesX = P.blocksX * 2;
+        const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
+        const int y = P.rowStart + r * P.rowStride;
+        const V3 pdir = primary_dir(P, x, y);
+        const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
+        unsigned L = 0;
+        for (int w = 0; w < P.maskWords; ++w)
+            L += (unsigned)__popcll(mask[w]);
+        Closest prim{999999.f, -1};
+        if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
+            primary_listed_lds(pdir, prim, mask, P.maskWords, sPF, sPX);
+            if (lane == 0) {
+                segTraced++;
+                segTests += L;
+            }
+        }
+#ifdef RTC_DIAG
+        if (lane == 0)
+            atomicAdd(&g_rtc_sect[15], 1ull); /* pixels */
+        unsigned diagRounds = 0;
+#endif
+        unsigned base = (unsigned)(x + y * P.width); /* main.c:95: the state before sample s0 */
+        unsigned D = 7;                              /* predicted draws per sample */
+        V3 acc{0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < P.spp && P.maxBounce > 0;) {
+            const int n = min(64, P.spp - s0);
+            const bool act = lane < n;
+            unsigned rng = rng_advance(base, D * (unsigned)lane);
+            const unsigned start = rng;
+            V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+            int bounce = 0;
+            unsigned draws = 0, calls = 0, traced = 0;
+            bool live = act;
+#ifdef RTC_DIAG
+            if (lane == 0)
+                atomicAdd(&g_rtc_sect[13], 1ull); /* rounds */
+            diagRounds++;
+#endif
+            while (__any(live)) {
+#ifdef RTC_DIAG
+                if (lane == 0)
+                    atomicAdd(&g_rtc_sect[14], 1ull); /* wave iterations */
+#endif
+                if (live) {
+                    Closest c;
+                    calls++;
+                    if (bounce == 0) {
+                        if (P.hoist) {
+                            c = prim;
+                        } else {
+                            c = Closest{999999.f, -1};
+                            primary_listed_lds(dir, c, mask, P.maskWords, sPF, sPX);
+                            traced++;
+                            segTests += L;
+                        }
+                    } else {
+                        unsigned tt = 0;
+                        c = trace_clusters(P, pos, dir, sTri, sCl, tt);
+                        traced++;
+                        segTests += tt;
+                        segClusters += (unsigned)P.clusterCount;
+                    }
+                    bool endSample;
+                    if (c.idx >= 0) {
+                        /* calcColor hit branch, raytracing.c:272-287 */
+                        const V3 hitPoint = add(pos, mul(dir, c.dst));
+                        const DevMat M = sShade[c.idx];
+                        const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+                        const V3 specularDir = reflect(dir, normal);
+                        dir = lerp(diffuseDir, specularDir, M.smoothness);
+                        pos = hitPoint;
+                        const V3 emitted = mul(color, M.emission);
+                        light = add(light, mulv(emitted, rayColor));
+                        rayColor = mulv(rayColor, color);
+                        const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                        endSample = p < random_value(rng);
+                        draws += 7;
+                        if (!endSample) {
+                            rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
+                            bounce++;
+                            endSample = bounce >= P.maxBounce;
+                        }
+                    } else {
+                        light = add(light, mulv(environment(dir, P.env), rayColor));
+                        endSample = true;
+                    }
+                    if (endSample)
+                        live = false;
+                }
+            }
+            /* lanes 0..f are correct: f = the first lane whose sample took other than D draws (or the last) */
+            const unsigned long long bad = __ballot(act && draws != D);
+            const int nv = bad ? min(__builtin_ctzll(bad) + 1, n) : n;
+            if (lane < nv) {
+                segCalls += calls;
+                segTraced += traced;
+            }
+            for (int j = 0; j < nv; ++j) { /* main.c:99, in sample order */
+                const V3 lj{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.x), j)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.y), j)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.z), j))};
+                acc = add(acc, mul(lj, P.invSpp));
+            }
+            const unsigned lastStart = (unsigned)__builtin_amdgcn_readlane((int)start, nv - 1);
+            const unsigned lastDraws = (unsigned)__builtin_amdgcn_readlane((int)draws, nv - 1);
+            base = rng_advance(lastStart, lastDraws);
+            /* the primary ray is every sample's: 0 draws if it misses, else mostly one hit (7 draws) */
+            D = lastDraws == 0u ? 0u : 7u;
+            s0 += nv;
+        }
+#ifdef RTC_DIAG
+        if (lane == 0)
+            atomicMax(&g_rtc_sect[12], (unsigned long long)diagRounds); /* max rounds of a pixel */
+#endif
+        if (lane == 0) {
+            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
+            P.colors[3 * o] = float_to_u8(acc.x);
+            P.colors[3 * o + 1] = float_to_u8(acc.y);
+            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (P.accum) {
+                P.accum[3 * o] = acc.x;
+                P.accum[3 * o + 1] = acc.y;
+                P.accum[3 * o + 2] = acc.z;
+            }
+        }
+    }
+    flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters);
+}
+
+__host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
+{
+    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX));
 }
 
 static EnvParams env_of(const Scene &s)
@@ -1975,7 +2279,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     if (cull) {
-        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int);
+        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int) +
+                            tiles * 64 * sizeof(int); /* + the geometry pixel list */
         if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (ms->scratch)
@@ -2014,6 +2319,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
             P.order = order;
             P.heavy = heavy;
+            const bool spec = (d->flags & RTC_F_SPEC) != 0;
+            if (spec) {
+                int *pixList = heavy + 4;
+                hipLaunchKernelGGL(rtc_pixel_list, dim3(1), dim3(1024), 0, st, (const int *)order, (const unsigned long long *)pixMask,
+                                   heavy, pixList);
+                P.pixList = pixList;
+            }
 #ifndef RTC_SIDE_STREAM
 #define RTC_SIDE_STREAM 1
 #endif
@@ -2034,7 +2346,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             /* small launches: 8 lanes per pixel (shorter chains; see KC) */
             const bool eight = (d->flags & RTC_F_COOP8) ||
                                (!(d->flags & RTC_F_COOP4) && (size_t)d->width * (size_t)rows <= (size_t)RTC_COOP8_MAX_PIXELS);
-            if (eight)
+            if (spec)
+                hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
+            else if (eight)
                 hipLaunchKernelGGL(rtc_render_heavy<8>, workers, dim3(64 * 8), rtc_heavy_lds_bytes(s->triPadded), st, P);
             else
                 hipLaunchKernelGGL(rtc_render_heavy<4>, workers, dim3(64 * 4), rtc_heavy_lds_bytes(s->triPadded), st, P);

@@ -143,6 +143,9 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
     # (primary segments always visit only the candidates in the cooperative path, even when other pixels of
     # the wave are on later bounces: fewer tests)
     assert s1["segments"] == s2["segments"] and s1["tri_tests"] <= s2["tri_tests"]
+    # the sample-parallel speculative kernel (RTC_F_SPEC): same bits, same segment counts
+    c4, a4, s4 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "spec": True}), want_accum=True)
+    assert np.array_equal(_bits(a1), _bits(a4)) and np.array_equal(c1, c4) and s1["segments"] == s4["segments"]
     # 4 and 8 cooperating lanes per pixel (RTC_F_COOP4 / RTC_F_COOP8): same bits, same counters
     for lanes in (4, 8):
         c3, a3, s3 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "coop_lanes": lanes}),

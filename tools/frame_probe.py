@@ -24,6 +24,7 @@ for name, t, cfg in [("empty", tris[:0], rt.RenderConfig(W, H, SPP, 10, True)),
                      ("faithful", tris, rt.RenderConfig(W, H, SPP, 10, True)),
                      ("faithful_nocluster", tris, rt.RenderConfig(W, H, SPP, 10, True, cluster_cull=False)),
                      ("faithful_nocoop", tris, rt.RenderConfig(W, H, SPP, 10, True, coop=False)),
+                     ("faithful_spec", tris, rt.RenderConfig(W, H, SPP, 10, True, spec=True)),
                      ("hoist", tris, rt.RenderConfig(W, H, SPP, 10, True, hoist=True))]:
     ds = rt.DeviceScene(t, None)
     times = []

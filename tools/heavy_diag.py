@@ -27,12 +27,13 @@ out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
 ds = rt.DeviceScene(tris, None)
 stream = torch.cuda.current_stream()
 rt.lib().rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
-sect = np.zeros(8, np.uint64)
+sect = np.zeros(16, np.uint64)
 NAMES = ["primary_trace", "cluster_tests", "gen_filter", "gen_exact", "lane_reduce", "hit_shading", "sky_miss",
          "loop_total"]
 STRIDE = int(os.environ.get("DIAG_STRIDE", "1"))
 for hoist in (False, True):
-    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, row_stride=STRIDE)
+    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, row_stride=STRIDE,
+                          spec=os.environ.get("DIAG_SPEC", "0") == "1")
     for rep in range(2):
         buf.zero_()
         rt.check(rt.lib().rtc_diag_sections(None, 1), "sections")
@@ -42,8 +43,11 @@ for hoist in (False, True):
         e1.record(stream)
         torch.cuda.synchronize()
     rt.check(rt.lib().rtc_diag_sections(sect.ctypes.data_as(C.c_void_p), 0), "sections")
-    tot = float(sect[7])
+    tot = max(float(sect[7]), 1.0)
     print(json.dumps({"hoist": hoist, "section_share_of_loop": {n: round(float(v) / tot, 3) for n, v in zip(NAMES, sect)},
+                      "samples": int(sect[8]), "non7_samples": int(sect[9]), "zero_hit_samples": int(sect[10]),
+                      "pixels": int(sect[11]), "max_non7_per_pixel": int(sect[12]),
+                      "spec_rounds": int(sect[13]), "spec_wave_iters": int(sect[14]), "spec_pixels": int(sect[15]),
                       "loop_cycles_per_wave": round(tot / (len(np.unique(buf.view(tiles, 4)[:, 3].cpu().numpy() >> 32)) * 4), 0)}))
     d = buf.view(tiles, 4).cpu().numpy()
     m = d[:, 1] > 0

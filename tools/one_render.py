@@ -15,7 +15,9 @@ tris, _ = load_tris("ultracomplex")
 cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True),
        "nocull": rt.RenderConfig(1920, 1080, 64, 10, True, tile_cull=False), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
        "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
-       "empty": rt.RenderConfig(1920, 1080, 64, 10, True)}[v]
+       "empty": rt.RenderConfig(1920, 1080, 64, 10, True),
+       "share8": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8),
+       "share8c4": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8, coop_lanes=4)}[v]
 if v == "empty":
     tris = tris[:0]
 for _ in range(reps):
