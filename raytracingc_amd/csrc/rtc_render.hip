@@ -1465,6 +1465,52 @@ __device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, const 
     return b > 0.f ? x2 > T2 * (rho * rho) : w2 > T2;
 }
 
+/* In-group lane exchanges by DPP (VALU lane moves, no LDS round trip; ds_bpermute costs a wait of ~100
+ * cycles each, exposed when few waves share a SIMD).  Groups are KC = 4 or 8 consecutive lanes whose lanes
+ * share control flow (the lanes of one pixel). */
+constexpr int kDppXor1 = 0xB1;       /* quad_perm(1,0,3,2) */
+constexpr int kDppXor2 = 0x4E;       /* quad_perm(2,3,0,1) */
+constexpr int kDppHalfMirror = 0x141; /* lane i <- lane 7-i within 8 */
+constexpr int kDppRowShl3 = 0x103;   /* lane i <- lane i+3 within a row of 16 */
+template <int CTRL> __device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+/* lane K (< 4) of this lane's group */
+template <int KC, int K> __device__ __forceinline__ float group_lane(float v, int sub)
+{
+    const float q = dpp_f<85 * K>(v); /* quad_perm(K,K,K,K) */
+    if constexpr (KC == 4) {
+        return q;
+    } else {
+        const float m = dpp_f<kDppHalfMirror>(q); /* lanes 4..7 take it from lanes 3..0 */
+        return sub < 4 ? q : m;
+    }
+}
+/* exchange partner for reduction step `step` (0: xor 1, 1: xor 2, 2: the other quad of 8) */
+template <int STEP> __device__ __forceinline__ int group_xchg_i(int v)
+{
+    return dpp_i<STEP == 0 ? kDppXor1 : (STEP == 1 ? kDppXor2 : kDppHalfMirror)>(v);
+}
+template <int KC> __device__ __forceinline__ unsigned group_or(unsigned v)
+{
+    v |= (unsigned)group_xchg_i<0>((int)v);
+    v |= (unsigned)group_xchg_i<1>((int)v);
+    if constexpr (KC == 8)
+        v |= (unsigned)group_xchg_i<2>((int)v);
+    return v;
+}
+template <int STEP> __device__ __forceinline__ void lex_min_step(Closest &c)
+{
+    const float od = __int_as_float(group_xchg_i<STEP>(__float_as_int(c.dst)));
+    const int oi = group_xchg_i<STEP>(c.idx);
+    if (od < c.dst || (od == c.dst && (unsigned)oi < (unsigned)c.idx)) {
+        c.dst = od;
+        c.idx = oi;
+    }
+}
+
 /* Position of the n-th (0-based) set bit of m; m must have more than n set bits. */
 __device__ __forceinline__ int nth_set_bit(unsigned long long m, int n)
 {
@@ -1527,9 +1573,7 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
         unsigned cm = 0;
         for (int k = sub; k < P.clusterCount; k += KC)
             cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, sCl[k])) << k;
-#pragma unroll
-        for (int k = 1; k < KC; k <<= 1)
-            cm |= (unsigned)__shfl_xor((int)cm, k);
+        cm = group_or<KC>(cm);
         /* triangles in the clusters kept (only the last cluster has zero records) */
         testedTris = (unsigned)__popc(cm) * kClusterSize -
                      ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
@@ -1555,15 +1599,11 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
         DSECT_END(d3, 3);
     }
     DSECT_BEGIN(d4);
-#pragma unroll
-    for (int k = 1; k < KC; k <<= 1) {
-        const float od = __shfl_xor(c.dst, k);
-        const int oi = __shfl_xor(c.idx, k);
-        if (od < c.dst || (od == c.dst && (unsigned)oi < (unsigned)c.idx)) {
-            c.dst = od;
-            c.idx = oi;
-        }
-    }
+    /* exact (dst, index) lexicographic minimum over the group */
+    lex_min_step<0>(c);
+    lex_min_step<1>(c);
+    if constexpr (KC == 8)
+        lex_min_step<2>(c);
     DSECT_END(d4, 4);
     return c;
 }
@@ -1606,23 +1646,28 @@ __device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int gr
             t = (double)(float)__builtin_sqrt(-2 * rtcmath::log((double)u));
         else
             t = rtcmath::cos((double)(float)(2 * 3.14159265 * (double)u));
-        const double c = __shfl(t, groupBase + 3 + (sub < 3 ? sub : 0));
+        /* lane k < 3 takes cos_k from lane k + 3 */
+        const long long tb = __double_as_longlong(t);
+        const int lo = dpp_i<kDppRowShl3>((int)(unsigned)tb), hi = dpp_i<kDppRowShl3>((int)(tb >> 32));
+        const double c = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
         n = (float)(t * c); /* valid on lanes 0..2: rho_k * cos_k */
     }
     s = s * j6.a + j6.c;
-    const float nx = __shfl(n, groupBase), ny = __shfl(n, groupBase + 1), nz = __shfl(n, groupBase + 2);
+    (void)groupBase;
+    const float nx = group_lane<KC, 0>(n, sub), ny = group_lane<KC, 1>(n, sub), nz = group_lane<KC, 2>(n, sub);
     return normalized(V3{nx, ny, nz});
 }
 
 /* getEnvironmentLight (raytracing.c:151-160) with its two powf calls on two lanes of the pixel's group */
-__device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub, int groupBase)
+template <int KC>
+__device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub)
 {
     const float sky = smoothstep(0.f, 0.74f, -dir.y);
     const float sunDot = fmaxf(0.f, dot(dir, s.sun));
     const bool second = (sub & 1) != 0;
     const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f, s);
-    const float skyGradientT = __shfl(pw, groupBase);
-    const float sunPow = __shfl(pw, groupBase + 1);
+    const float skyGradientT = group_lane<KC, 0>(pw, sub);
+    const float sunPow = group_lane<KC, 1>(pw, sub);
     const V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
     const float sun = sunPow * s.intensity;
     const float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
@@ -1852,7 +1897,7 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
                     DSECT_END(d5, 5);
                 } else {
                     DSECT_BEGIN(d6);
-                    light = add(light, mulv(environment_coop(dir, P.env, sub, groupBase), rayColor));
+                    light = add(light, mulv(environment_coop<KC>(dir, P.env, sub), rayColor));
                     endSample = true;
                     DSECT_END(d6, 6);
                 }
