@@ -671,6 +671,25 @@ __device__ __forceinline__ void primary_exact(const RenderParams &P, V3 dir, con
     }
 }
 
+/* primary_exact with the DevPrimX record at hand (LDS-staged in the cooperative kernel) */
+__device__ __forceinline__ void primary_exact_x(V3 dir, const DevPrimF &F, const DevPrimX &X, int t, Closest &c)
+{
+    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
+        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
+        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
+        if (!(-kEps < det && det < kEps)) {
+            const float invDet = rcp_cr(det); /* IEEE 1.f / det */
+            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
+            const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
+            const float dst = X.dac0 * invDet;
+            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
+                c.dst = dst;
+                c.idx = t;
+            }
+        }
+    }
+}
+
 /* One primary record (see closest_primary). */
 __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
                                              Closest &c)
@@ -1537,7 +1556,8 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, int n)
 template <int KC>
 __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 dir, bool primarySeg,
                                               const DevTri *__restrict__ sTri, const DevCluster *__restrict__ sCl,
-                                              const DevPrimF *__restrict__ sPrimF, const int *__restrict__ sCand,
+                                              const DevPrimF *__restrict__ sPrimF, const DevPrimX *__restrict__ sPrimX,
+                                              const int *__restrict__ sCand,
                                               int L, int sub, unsigned &testedTris)
 {
     Closest c{999999.f, -1};
@@ -1559,7 +1579,7 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
             const int b = __builtin_ctzll(surv);
             surv &= surv - 1;
             const int k = sub + KC * b;
-            primary_exact(P, dir, sPrimF[k], sCand[k], 0, c);
+            primary_exact_x(dir, sPrimF[k], sPrimX[k], sCand[k], c);
         }
         DSECT_END(d0, 0);
     } else {
@@ -1741,7 +1761,7 @@ constexpr int kHeavyWorkers = 2048;
 constexpr bool kPrimaryList = RTC_COOP_PRIMARY_LIST != 0;
 __host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
 {
-    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(int)) + 16;
+    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX) + sizeof(int)) + 16;
 }
 
 #ifndef RTC_HEAVY_WAVES
@@ -1756,7 +1776,8 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
     DevTri *sTri = (DevTri *)sDyn;
     DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
     DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
-    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
+    DevPrimX *sPrimX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
+    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat) + sizeof(DevPrimX)));
     int &sCount = sCand[P.triPadded];
     __shared__ int sItem;
     __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
@@ -1835,7 +1856,10 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
         __syncthreads();
         L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
         for (int k = threadIdx.x; k < (int)L; k += (64 * KC))
+        {
             sPrimF[k] = P.primF[sCand[k]];
+            sPrimX[k] = P.primX[sCand[k]];
+        }
         __syncthreads();
         }
 
@@ -1847,7 +1871,7 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
         Closest primary{999999.f, -1};
         if (P.hoist && alive) {
             unsigned nc = 0;
-            primary = coop_trace<KC>(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+            primary = coop_trace<KC>(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
             segTraced++;
             segTests += kPrimaryList ? L : nc;
             segClusters += kPrimaryList ? 0u : (unsigned)P.clusterCount;
@@ -1865,7 +1889,7 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
                 } else {
                     unsigned nc = 0;
                     const bool listed = kPrimaryList && bounce == 0;
-                    c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sCand, (int)L, sub, nc);
+                    c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
                     segTraced++;
                     segTests += listed ? L : nc;
                     segClusters += listed ? 0u : (unsigned)P.clusterCount;
