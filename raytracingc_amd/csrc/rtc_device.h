@@ -153,6 +153,10 @@ struct EnvParams {
 
 __device__ __forceinline__ float pow_ref(float x, float y, const EnvParams &s)
 {
+    /* the environment's x is smoothstep's [0, 1] or fmax(0, .) (or NaN) and y a launch constant: the
+     * branch-free variant, unless y is special or x has its sign bit set (-0, negative) */
+    if (!rtcmath::powf_zeroinfnan(rtcmath::f2u(y)) && (!(rtcmath::f2u(x) >> 31) || x != x))
+        return s.log2tab ? rtcmath::powf_glibc_pos<true>(x, y, s.log2tab, s.exp2tab) : rtcmath::powf_glibc_pos<true>(x, y);
     return s.log2tab ? rtcmath::powf_glibc<true>(x, y, s.log2tab, s.exp2tab) : rtcmath::powf_glibc<true>(x, y);
 }
 

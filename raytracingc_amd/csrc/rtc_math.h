@@ -385,6 +385,31 @@ RTC_HD float powf_glibc(float x, float y, const double (*log2tab)[2] = powf_data
     return powf_exp2<FMA>(ylogx, signBias, exp2tab);
 }
 
+/* powf_glibc for the environment's arguments, branch-free: x with the sign bit clear (+0, subnormal, normal,
+ * +inf or NaN) and y finite and nonzero.  The main path runs for every x (bounded table indices whatever
+ * the bits) and glibc's special results are selected over it: x = +0 -> 0 (1/0 = inf for y < 0), NaN ->
+ * x*x (1/(x*x) for y < 0), +inf -> inf (0 for y < 0), subnormal x normalised first, the over/underflow
+ * limits of the exp2 step.  Bit-identical to powf_glibc on every such x (tools/exact_probe.hip). */
+template <bool FMA>
+RTC_HD float powf_glibc_pos(float x, float y, const double (*log2tab)[2] = powf_data::kLog2Tab,
+                            const unsigned long long *exp2tab = powf_data::kExp2Tab)
+{
+    const unsigned ix = f2u(x), iy = f2u(y);
+    const bool sub = ix < 0x00800000u;
+    const unsigned ixs = (f2u(x * 0x1p23f) & 0x7fffffffu) - (23u << 23);
+    const double logx = powf_log2<FMA>(sub ? ixs : ix, log2tab);
+    const double ylogx = (double)y * logx;
+    float r = powf_exp2<FMA>(ylogx, 0u, exp2tab);
+    r = ylogx > 0x1.fffffffd1d571p+6 ? __builtin_inff() : r;
+    r = ylogx <= -150.0 ? 0.0f : r;
+    const bool yneg = (iy & 0x80000000u) != 0;
+    const float x2 = x * x;
+    r = ix == 0u ? (yneg ? __builtin_inff() : 0.0f) : r;
+    r = ix == 0x7f800000u ? (yneg ? 0.0f : __builtin_inff()) : r;
+    r = ix > 0x7f800000u ? (yneg ? 1.0f / x2 : x2) : r;
+    return r;
+}
+
 /* powf(x, y) of raytracing.c:153,155 for x >= 0 (or NaN): exp2(y * log2(x)) in double, rounded once */
 RTC_HD float pow_ref(float x, float y)
 {

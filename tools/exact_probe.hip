@@ -2,6 +2,8 @@
 // all 2^32 float bit patterns (test infrastructure; tests/test_gpu_exact.py runs it, `make probe` builds it):
 //   sqrt_cr(x)  == (float)sqrt((double)x)        (length(), moremath.c:9)
 //   rcp_cr(x)   == 1.f / x  (IEEE f32 divide)     (normalized(), moremath.c:14; (float)(1./x) == 1.f/x)
+//   powf_glibc_pos(x, y) == powf_glibc(x, y) bit for bit, every x with the sign bit clear, y in kPowY
+//                                                 (getEnvironmentLight's powf, raytracing.c:153,155)
 // Prints one line per check: "<name> mismatches <n> checked <m>".  Exit status 0 iff every count is 0.
 #include <hip/hip_runtime.h>
 
@@ -36,23 +38,44 @@ __global__ void check(unsigned long long base, unsigned long long *bad)
     }
 }
 
+__constant__ float kPowY[8] = {0.35f, 22.f, 7.5f, 1.3f, 0.5f, -3.f, 150.f, 1e-5f};
+
+__global__ void check_pow(unsigned long long base, unsigned long long *bad)
+{
+    const unsigned long long i = base + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    const float x = __uint_as_float((unsigned)i); /* i < 2^31: sign bit clear */
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float y = kPowY[k];
+        if (__float_as_uint(rtcmath::powf_glibc_pos<true>(x, y)) != __float_as_uint(rtcmath::powf_glibc<true>(x, y)))
+            b++;
+    }
+    const unsigned long long m = __ballot(b != 0);
+    if ((threadIdx.x & 63) == 0 && m)
+        atomicAdd(&bad[2], (unsigned long long)__popcll(m));
+}
+
 int main()
 {
     unsigned long long *bad;
-    if (hipMalloc(&bad, 2 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&bad, 3 * sizeof(unsigned long long)) != hipSuccess) {
         printf("no device\n");
         return 2;
     }
-    (void)hipMemset(bad, 0, 2 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 3 * sizeof(unsigned long long));
     const unsigned long long chunk = 1ull << 30;
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
-    unsigned long long h[2] = {0, 0};
+    for (unsigned long long base = 0; base < (1ull << 31); base += chunk)
+        hipLaunchKernelGGL(check_pow, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
+    unsigned long long h[3] = {0, 0, 0};
     if (hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
         printf("copy failed\n");
         return 2;
     }
     printf("sqrt_cr mismatches %llu checked %llu\n", h[0], 1ull << 32);
     printf("rcp_cr mismatches %llu checked %llu\n", h[1], 1ull << 32);
-    return (h[0] | h[1]) ? 1 : 0;
+    printf("powf_glibc_pos mismatches %llu checked %llu\n", h[2], 8ull << 31);
+    return (h[0] | h[1] | h[2]) ? 1 : 0;
 }
