@@ -2,9 +2,10 @@
 
 Bar (BASELINE.json north_star): per-channel |delta| <= 1e-4 on the pre-quantisation float framebuffer (NaN == NaN);
 we also assert that no pixel exceeds it, that the traced segment count (paths) is identical, and we report
-the uint8 mismatch count.  Integer / index work (RNG, hit tests, hit distances) is bit-exact.  The one known
-source of float differences is powf (glibc's powf is within 0.82 ulp; the device evaluates it in double and
-rounds once, see rtc_device.h), which touches only the terminal environment lookup.
+the uint8 mismatch count.  Integer / index work (RNG, hit tests, hit distances) is bit-exact.  The device
+powf restates glibc's own algorithm (rtc_math.h), so whole frames are bit-identical to the reference except
+NaN sign bits on height-1 frames (every direction NaN); every shortcut of the GPU path (tile lists, clusters,
+cooperative lanes, hoisting, speculation) is checked bit-exact against its brute-force counterpart.
 """
 from __future__ import annotations
 
