@@ -142,9 +142,12 @@ int rtc_rows_selected(const RtcRenderDesc *d);
  * A scene handle serves one stream at a time: its per-launch scratch (primary-ray records, tile candidate
  * lists) is rewritten by every launch. */
 #define RTC_SEGMENT_COUNTERS 4
-/* Device times (ms) of the last rtc_render_rows_async on s, per kernel of the split launch: out[0] the
- * heavy-tile kernel, out[1] the sky kernel (concurrent, on the scene's side stream); -1 when the last launch
- * was not a split launch.  Waits for that launch to finish. */
+/* Per-kernel timing of the split launch: with rtc_scene_set_timing(s, 1) every later launch on s records HIP
+ * events around its two kernels (off by default: the records cost each launch a few microseconds), and
+ * rtc_scene_kernel_times returns the device times (ms) of the last launch: out[0] the heavy-tile kernel,
+ * out[1] the sky kernel (concurrent, on the scene's side stream); -1 when that launch recorded none.  Waits
+ * for that launch to finish. */
+int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,

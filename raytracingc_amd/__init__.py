@@ -218,6 +218,10 @@ class DeviceScene:
                                           C.c_void_p(segments_ptr) if segments_ptr else None,
                                           C.c_void_p(stream) if stream else None), "rtc_render_rows_async")
 
+    def set_timing(self, enable: bool):
+        """Record HIP events around the split launch's kernels from now on (rtc_scene_set_timing)."""
+        check(lib().rtc_scene_set_timing(self._h, int(enable)), "rtc_scene_set_timing")
+
     def kernel_times(self):
         """(heavy-tile kernel ms, sky kernel ms) of the last split launch (None if it was not one)."""
         out = (C.c_float * 2)()

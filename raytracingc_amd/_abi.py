@@ -117,7 +117,7 @@ EXPORTS = [
     "rtc_load_obj", "rtc_parse_triangle_file", "rtc_free", "rtc_default_spheres", "rtc_default_scene",
     "rtc_scene_set_sun", "rtc_camera_basis", "rtc_write_bmp", "rtc_quantize",
     "rtc_render", "rtc_render_multi",
-    "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_kernel_times",
+    "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_deinterleave_async",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
@@ -168,6 +168,7 @@ def lib() -> C.CDLL:
     L.rtc_scene_upload.argtypes = [vp, ip, vp, ip, ip, C.POINTER(vp)]
     L.rtc_scene_release.argtypes = [vp]
     L.rtc_scene_kernel_times.argtypes = [vp, vp]
+    L.rtc_scene_set_timing.argtypes = [vp, C.c_int]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]
     L.rtc_render_rows_async.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp,
                                         vp, vp]

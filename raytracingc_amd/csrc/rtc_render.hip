@@ -172,7 +172,8 @@ struct RtcDeviceScene {
     hipEvent_t evFork, evJoin;
     /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
     hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
-    bool timed; /* the last launch was a split launch that recorded them */
+    bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
+    bool timed;  /* the last launch was a split launch that recorded them */
 };
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
@@ -379,6 +380,8 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipMalloc(&s->primX, dt.size() * sizeof(DevPrimX));
     if (e == hipSuccess)
         e = hipMalloc(&s->segSlots, 256 * 16 * sizeof(unsigned long long));
+    if (e == hipSuccess) /* kept zero between launches by rtc_reduce_segments */
+        e = hipMemset(s->segSlots, 0, 256 * 16 * sizeof(unsigned long long));
     if (e == hipSuccess)
         e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -1148,7 +1151,7 @@ __device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned s
     }
 }
 
-__global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(const unsigned long long *__restrict__ slots,
+__global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(unsigned long long *__restrict__ slots,
                                                                  unsigned long long *__restrict__ out)
 {
     __shared__ unsigned long long part[4][kSegSlots / 64];
@@ -1156,6 +1159,7 @@ __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(const unsigned 
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         unsigned long long v = slots[(size_t)t * kSegSlotStride + k];
+        slots[(size_t)t * kSegSlotStride + k] = 0; /* zero again for the next launch */
         for (int off = 32; off > 0; off >>= 1)
             v += __shfl_xor(v, off);
         if (lane == 0)
@@ -2361,8 +2365,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         }
     }
     P.blocksX = (int)grid.x;
-    if (dSegments)
-        HIP_TRY(hipMemsetAsync(s->segSlots, 0, kSegSlots * kSegSlotStride * sizeof(unsigned long long), st));
+    /* (the counter slots are zero here: rtc_scene_upload clears them, rtc_reduce_segments re-zeroes them) */
     auto finish = [&]() -> int {
         if (dSegments) {
             hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
@@ -2404,13 +2407,16 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
             }
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
-            HIP_TRY(hipEventRecord(s->evSky0, skyStream));
+            if (s->timing)
+                HIP_TRY(hipEventRecord(s->evSky0, skyStream));
             hipLaunchKernelGGL(rtc_render_sky, grid, dim3(kBlock), 0, skyStream, P, (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(s->evSky1, skyStream));
+            if (s->timing)
+                HIP_TRY(hipEventRecord(s->evSky1, skyStream));
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
-            HIP_TRY(hipEventRecord(s->evHeavy0, st));
+            if (s->timing)
+                HIP_TRY(hipEventRecord(s->evHeavy0, st));
             const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
             /* small launches: 8 lanes per pixel (shorter chains; see KC) */
             const bool eight = (d->flags & RTC_F_COOP8) ||
@@ -2422,8 +2428,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             else
                 hipLaunchKernelGGL(rtc_render_heavy<4>, workers, dim3(64 * 4), rtc_heavy_lds_bytes(s->triPadded), st, P);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(s->evHeavy1, st));
-            ms->timed = true;
+            if (s->timing)
+                HIP_TRY(hipEventRecord(s->evHeavy1, st));
+            ms->timed = s->timing;
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
             return finish();
@@ -2934,6 +2941,14 @@ extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const
         rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
     rtc_scene_release(s);
     return rc;
+}
+
+extern "C" int rtc_scene_set_timing(RtcDeviceScene *s, int enable)
+{
+    if (!s)
+        return rtc_fail(RTC_EINVAL, "rtc_scene_set_timing: null scene");
+    s->timing = enable != 0;
+    return 0;
 }
 
 extern "C" int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2])

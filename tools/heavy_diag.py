@@ -25,6 +25,7 @@ rt.lib().rtc_diag_set_buffer.argtypes = [C.c_void_p]
 rt.check(rt.lib().rtc_diag_set_buffer(C.c_void_p(buf.data_ptr())), "diag")
 out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
 ds = rt.DeviceScene(tris, None)
+ds.set_timing(True)
 stream = torch.cuda.current_stream()
 rt.lib().rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
 sect = np.zeros(16, np.uint64)

@@ -19,6 +19,7 @@ tris, _ = load_tris("ultracomplex")
 scene, cam = rt.default_scene(), rt.camera_basis()
 W, H, SPP = 1920, 1080, 64
 ds = rt.DeviceScene(tris, None)
+ds.set_timing(True)
 stream = torch.cuda.current_stream()
 out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
 seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
