@@ -248,6 +248,9 @@ def main():
                          "hbm_achieved_gbs": round(alg_bytes / (dom_ms * 1e-3) / 1e9, 3),
                          "hbm_peak_gbs": HBM_PEAK_GBS,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
+                         # SURVEY.md §8(d)'s formula: segments_traced x T x 57 / (t x 157.3e12 x G); above 1
+                         # because the culling layers skip ~99 % of the brute-force tests (bit-exactly)
+                         "survey_formula_frac": round(bf_tf / FP32_VALU_PEAK_TFLOPS, 4),
                          "note": "achieved: the ray-triangle tests evaluated x 57 flop / the heavy-tile kernel's "
                                  "device time (HIP events around it); launch_ms: the whole launch sequence (cull, "
                                  "order, sky || heavy, counters); bruteforce_equiv: segments x T (the reference's "
