@@ -267,6 +267,48 @@ def test_row_partition_and_deinterleave(gpu_available):
     ds.close()
 
 
+def test_device_scene_reuse_sizes_counters_timing(gpu_available):
+    """One device-resident scene across launches of growing and shrinking frames (per-launch scratch regrown,
+    counter slots re-zeroed by the reduce kernel): every frame and segment count equals a fresh rtc_render;
+    the opt-in per-kernel timing reports positive times only while enabled."""
+    import torch
+
+    tris, tonly = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    ds = rt.DeviceScene(tris, None)
+    stream = torch.cuda.current_stream().cuda_stream
+    seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
+    for k, (W, H) in enumerate([(64, 36), (200, 120), (33, 17), (200, 120)]):
+        cfg = rt.RenderConfig(W, H, 4, 10, True)
+        ref, _, st = rt.render(tris, None, scene, cam, cfg)
+        out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+        seg.zero_()
+        ds.set_timing(k % 2 == 1)
+        ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, seg.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref), (W, H)
+        assert int(seg[0]) == st["segments"] and int(seg[2]) == st["tri_tests"], (W, H)
+        kt = ds.kernel_times()
+        if k % 2 == 1:
+            assert kt is not None and kt[0] > 0 and kt[1] > 0
+        else:
+            assert kt is None
+    ds.close()
+
+
+@pytest.mark.parametrize("variant", [{}, {"coop_lanes": 4}, {"coop_lanes": 8}, {"spec": True}, {"hoist": True}])
+def test_spp_not_multiple_of_64(variant, gpu_available):
+    """spp = 100 (the speculative kernel's two rounds of 64 and 36 samples, the cooperative kernels' chains)
+    against the oracle, bit for bit, with identical segment counts."""
+    tris, tonly = load_tris("complex")
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(48, 30, 100, 10, True, **variant)
+    col, acc, st = rt.render(tris, None, scene, cam, cfg, want_accum=True)
+    ocol, oacc, oseg = orc.render(tris, None, scene, cam, RtcRenderDesc(48, 30, 100, 10, tonly, 0, 1, 0), threads=16)
+    assert np.array_equal(_bits(acc), _bits(oacc)) and np.array_equal(col, ocol)
+    assert st["segments"] == oseg
+
+
 def test_render_multi_single_device_equals_render(gpu_available):
     tris, tonly = load_tris("complex")
     scene, cam, _ = setup_from_flags({})
