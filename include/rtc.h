@@ -66,6 +66,9 @@ typedef struct RtcRenderDesc {
 #define RTC_F_COOP4         0x40 /* force 4 cooperating lanes per pixel (default: 8 for launches of at most
                                     700k pixels, else 4; identical frame) */
 #define RTC_F_COOP8         0x80 /* force 8 cooperating lanes per pixel (identical frame) */
+#define RTC_F_PIPE          0x200 /* force the two-samples-in-flight kernel for tiles with geometry (default for
+                                     faithful launches of at most 1.1M pixels; identical frame) */
+#define RTC_F_NO_PIPE       0x400 /* never use it */
 #define RTC_F_SPEC          0x100 /* tiles with geometry: the sample-parallel speculative kernel (lanes = samples,
                                      RNG states jumped ahead and verified; identical frame) instead of the
                                      cooperative kernel (lanes split each segment) */

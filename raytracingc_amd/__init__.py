@@ -30,6 +30,8 @@ from ._abi import (  # noqa: F401
     RTC_F_COOP8,
     RTC_F_NO_CLUSTER_CULL,
     RTC_F_NO_COOP,
+    RTC_F_NO_PIPE,
+    RTC_F_PIPE,
     RTC_F_SPEC,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
@@ -139,13 +141,15 @@ class RenderConfig:
     cluster_cull: bool = True  # bounce rays skip triangle clusters they provably miss (same frame)
     coop_lanes: int = 0  # cooperating lanes per pixel in heavy tiles: 0 = by launch size, 4 or 8 (same frame)
     spec: bool = False  # heavy tiles: sample-parallel speculative kernel instead of the cooperative one (same frame)
+    pipe: int = 0  # two samples in flight per pixel: 0 = by launch size, 1 = force, -1 = never (same frame)
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
                 | (RTC_F_COOP4 if self.coop_lanes == 4 else 0) | (RTC_F_COOP8 if self.coop_lanes == 8 else 0)
-                | (RTC_F_SPEC if self.spec else 0))
+                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe > 0 else 0)
+                | (RTC_F_NO_PIPE if self.pipe < 0 else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),

@@ -1434,6 +1434,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
 #ifndef RTC_COOP8_MAX_PIXELS
 #define RTC_COOP8_MAX_PIXELS 700000
 #endif
+/* faithful launches up to this many pixels use rtc_render_pipe (two samples in flight per pixel): a rank's
+ * share of a multi-GPU 1080p or 4K frame; measured faster there, slower on a whole 1080p frame */
+#ifndef RTC_PIPE_MAX_PIXELS
+#define RTC_PIPE_MAX_PIXELS 1100000
+#endif
 #ifndef RTC_SKY_UNROLL
 #define RTC_SKY_UNROLL 2
 #endif
@@ -2277,6 +2282,239 @@ __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
     return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX));
 }
 
+
+/* ---- two samples in flight per pixel (rtc_render_pipe) ----------------------------------------------------
+ * A pixel's samples are chained only through the RNG state (main.c:95-100).  Here each pixel has two 4-lane
+ * groups: the current one runs sample n from its known start state, the speculative one runs sample n+1
+ * from the current start state advanced by D draws (rng_advance; D = 7, a single hit, or 0 when the primary
+ * ray misses).  When the current sample ends, its radiance is accumulated (main.c:99, in sample order) and
+ * the speculative sample is kept if and only if it started from exactly the state the current one ended in
+ * (then it is the reference's sample n+1, whatever path led there); otherwise it restarts from that state.
+ * Every accumulated sample is therefore the reference's; the chain of a pixel is about half as long.  Used
+ * for small faithful launches (a rank's share of a multi-GPU frame), where chains, not issue, bound the time. */
+__device__ __forceinline__ int pipe_other_i(int v) { return dpp_i<kDppHalfMirror>(v); } /* lane i <- 7-i of 8 */
+__device__ __forceinline__ float pipe_other_f(float v) { return dpp_f<kDppHalfMirror>(v); }
+
+__global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
+{
+    constexpr int KC = 4, kThreads = 512;
+    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
+    __shared__ PowTablesLds sPow;
+    DevTri *sTri = (DevTri *)sDyn;
+    DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
+    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
+    DevPrimX *sPrimX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
+    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat) + sizeof(DevPrimX)));
+    int &sCount = sCand[P.triPadded];
+    __shared__ int sItem;
+    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
+    sPow.fill(threadIdx.x);
+    sPow.attach(P.env);
+    for (int i = threadIdx.x; i < P.triPadded; i += kThreads)
+        sTri[i] = P.clTris[i];
+    for (int i = threadIdx.x; i < P.clusterCount; i += kThreads)
+        sCl[i] = P.clusters[i];
+    for (int i = threadIdx.x; i < P.triPadded; i += kThreads) {
+        DevMat m = P.mats[i];
+        const DevTri &t = P.tris[i];
+        m.pad0 = t.nx;
+        m.pad1 = t.ny;
+        m.pad2 = t.nz;
+        sShade[i] = m;
+    }
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & (KC - 1);
+    const int groupBase = lane & ~(KC - 1);
+    const int g = (lane >> 2) & 1; /* which of the pixel's two groups */
+    unsigned segCalls = 0, segTraced = 0, segClusters = 0;
+    unsigned long long segTests = 0;
+    const int heavy = P.heavy[0];
+    for (;;) {
+        if (threadIdx.x == 0)
+            sItem = atomicAdd(&P.heavy[1], 1);
+        __syncthreads();
+        const int slot = __builtin_amdgcn_readfirstlane(sItem);
+        if (slot >= heavy)
+            break;
+        const int tile = P.order[slot];
+        const int wave = threadIdx.x >> 6;
+        const int tilesX = P.blocksX * 2;
+        const int tx = tile % tilesX, ty = tile / tilesX;
+        const unsigned long long geo = P.pixMask[tile];
+        const int slotPx = wave * 8 + lane / 8;
+        const bool valid = slotPx < __popcll(geo);
+        const int pi = nth_set_bit(geo, valid ? slotPx : 0);
+        const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
+        const int y = P.rowStart + r * P.rowStride;
+        const V3 pdir = primary_dir(P, x, y);
+        if (wave == 0) {
+            const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
+            int base = 0;
+            for (int w = 0; w < P.maskWords; ++w) {
+                const unsigned long long m = mask[w];
+                if ((m >> lane) & 1ull)
+                    sCand[base + __popcll(m & ((1ull << lane) - 1ull))] = w * 64 + lane;
+                base += __popcll(m);
+            }
+            if (lane == 0)
+                sCount = base;
+        }
+        __syncthreads();
+        const unsigned L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
+        for (int k = threadIdx.x; k < (int)L; k += kThreads) {
+            sPrimF[k] = P.primF[sCand[k]];
+            sPrimX[k] = P.primX[sCand[k]];
+        }
+        __syncthreads();
+
+        /* this group's sample */
+        int n = -1;
+        unsigned st0 = 0, rng = 0, draws = 0, calls = 0, traced = 0;
+        int fin = 1, isCur = g == 0, bounce = 0;
+        V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+        auto start = [&](int ns, unsigned s0) {
+            if (ns < P.spp) {
+                n = ns;
+                st0 = rng = s0;
+                fin = 0;
+            } else {
+                n = -1;
+                fin = 1;
+            }
+            draws = calls = traced = 0;
+            bounce = 0;
+            pos = P.origin;
+            dir = pdir;
+            rayColor = V3{1.f, 1.f, 1.f};
+            light = V3{0.f, 0.f, 0.f};
+        };
+        /* the pixel (replicated on its 8 lanes) */
+        V3 acc{0.f, 0.f, 0.f};
+        unsigned pixCalls = 0, pixTraced = 0;
+        int committed = 0;
+        bool pixDone = !(valid && P.spp > 0 && P.maxBounce > 0);
+        if (!pixDone) {
+            const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
+            if (g == 0)
+                start(0, seed);
+            else
+                start(1, rng_advance(seed, 7u));
+        }
+        while (__any(!pixDone)) {
+            if (!pixDone && n >= 0 && !fin) {
+                /* one calculateRayCollision + calcColor step of this group's sample (as rtc_render_heavy) */
+                Closest c;
+                calls++;
+                unsigned nc = 0;
+                const bool listed = bounce == 0;
+                c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
+                traced++;
+                if (sub == 0) {
+                    segTests += listed ? L : nc;
+                    segClusters += listed ? 0u : (unsigned)P.clusterCount;
+                }
+                bool endSample;
+                if (c.idx >= 0) {
+                    const V3 hitPoint = add(pos, mul(dir, c.dst));
+                    const DevMat M = sShade[c.idx];
+                    const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
+                    const V3 diffuseDir = normalized(add(normal, random_direction_coop<KC>(rng, sub, groupBase)));
+                    const V3 specularDir = reflect(dir, normal);
+                    dir = lerp(diffuseDir, specularDir, M.smoothness);
+                    pos = hitPoint;
+                    const V3 emitted = mul(color, M.emission);
+                    light = add(light, mulv(emitted, rayColor));
+                    rayColor = mulv(rayColor, color);
+                    const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                    endSample = p < random_value(rng);
+                    draws += 7;
+                    if (!endSample) {
+                        rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
+                        bounce++;
+                        endSample = bounce >= P.maxBounce;
+                    }
+                } else {
+                    light = add(light, mulv(environment_coop<KC>(dir, P.env, sub), rayColor));
+                    endSample = true;
+                }
+                if (endSample)
+                    fin = 1;
+            }
+            /* the other group's sample (every lane of the wave takes part in the exchange) */
+            const int oN = pipe_other_i(n), oFin = pipe_other_i(fin), oCur = pipe_other_i(isCur);
+            const unsigned oSt0 = (unsigned)pipe_other_i((int)st0), oRng = (unsigned)pipe_other_i((int)rng);
+            const unsigned oDraws = (unsigned)pipe_other_i((int)draws), oCalls = (unsigned)pipe_other_i((int)calls),
+                           oTraced = (unsigned)pipe_other_i((int)traced);
+            const V3 oLight{pipe_other_f(light.x), pipe_other_f(light.y), pipe_other_f(light.z)};
+            (void)oCur;
+            const bool me = isCur != 0;
+            const int cN = me ? n : oN, cFin = me ? fin : oFin;
+            if (!pixDone && cFin && cN >= 0) {
+                const unsigned cRng = me ? rng : oRng, cDraws = me ? draws : oDraws;
+                const V3 cLight = me ? light : oLight;
+                const int sN = me ? oN : n, sFin = me ? oFin : fin;
+                const unsigned sSt0 = me ? oSt0 : st0, sRng = me ? oRng : rng, sDraws = me ? oDraws : draws;
+                const V3 sLight = me ? oLight : light;
+                acc = add(acc, mul(cLight, P.invSpp)); /* main.c:99: sample cN */
+                pixCalls += me ? calls : oCalls;
+                pixTraced += me ? traced : oTraced;
+                committed++;
+                unsigned e = cRng, D = cDraws == 0u ? 0u : 7u;
+                const bool sValid = sN == cN + 1 && sSt0 == e;
+                if (sValid && sFin) {
+                    acc = add(acc, mul(sLight, P.invSpp)); /* sample cN + 1 */
+                    pixCalls += me ? oCalls : calls;
+                    pixTraced += me ? oTraced : traced;
+                    committed++;
+                    e = sRng;
+                    D = sDraws == 0u ? 0u : 7u;
+                    if (g == 0) {
+                        start(sN + 1, e);
+                        isCur = 1;
+                    } else {
+                        start(sN + 2, rng_advance(e, D));
+                        isCur = 0;
+                    }
+                } else if (sValid) {
+                    /* the speculative sample is the current one now; the finished group runs the next */
+                    if (me) {
+                        start(sN + 1, rng_advance(sSt0, D));
+                        isCur = 0;
+                    } else {
+                        isCur = 1;
+                    }
+                } else {
+                    /* mispredicted (or none): the other group restarts sample cN + 1 from the true state */
+                    if (!me) {
+                        start(cN + 1, e);
+                        isCur = 1;
+                    } else {
+                        start(cN + 2, rng_advance(e, D));
+                        isCur = 0;
+                    }
+                }
+                if (committed >= P.spp)
+                    pixDone = true;
+            }
+        }
+        if (valid && g == 0 && sub == 0) {
+            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
+            P.colors[3 * o] = float_to_u8(acc.x);
+            P.colors[3 * o + 1] = float_to_u8(acc.y);
+            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (P.accum) {
+                P.accum[3 * o] = acc.x;
+                P.accum[3 * o + 1] = acc.y;
+                P.accum[3 * o + 2] = acc.z;
+            }
+            segCalls += pixCalls;
+            segTraced += pixTraced;
+        }
+        __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
+    }
+    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
+}
+
 static EnvParams env_of(const Scene &s)
 {
     EnvParams e{};
@@ -2421,8 +2659,12 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             /* small launches: 8 lanes per pixel (shorter chains; see KC) */
             const bool eight = (d->flags & RTC_F_COOP8) ||
                                (!(d->flags & RTC_F_COOP4) && (size_t)d->width * (size_t)rows <= (size_t)RTC_COOP8_MAX_PIXELS);
+            const bool pipe = !(d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_NO_PIPE)) && !P.hoist &&
+                              ((d->flags & RTC_F_PIPE) || (size_t)d->width * (size_t)rows <= (size_t)RTC_PIPE_MAX_PIXELS);
             if (spec)
                 hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
+            else if (pipe)
+                hipLaunchKernelGGL(rtc_render_pipe, workers, dim3(512), rtc_heavy_lds_bytes(s->triPadded), st, P);
             else if (eight)
                 hipLaunchKernelGGL(rtc_render_heavy<8>, workers, dim3(64 * 8), rtc_heavy_lds_bytes(s->triPadded), st, P);
             else

@@ -26,7 +26,7 @@ seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
 base = None
 for n in (1, 2, 4, 8):
     for r, lanes in [(0, 0), (0, -1)]:
-        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, spec=lanes == 0)
+        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, pipe=1 if lanes == 0 else -1)
         times, kts = [], []
         for _ in range(frames):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -40,7 +40,7 @@ for n in (1, 2, 4, 8):
         if n == 1 and base is None:
             base = ms
         heavy = sorted(k[0] for k in kts if k)[len(kts) // 2] if any(kts) else None
-        print(json.dumps({"n": n, "rank": r, "kernel": "spec" if lanes == 0 else "coop", "ms_median": round(ms, 3), "heavy_ms": round(heavy, 3) if heavy else None,
+        print(json.dumps({"n": n, "rank": r, "kernel": "pipe" if lanes == 0 else "coop", "ms_median": round(ms, 3), "heavy_ms": round(heavy, 3) if heavy else None,
                           "ideal_ms": round(base / n, 3), "efficiency_if_only_this": round(base / n / ms, 3)}),
               flush=True)
 ds.close()
