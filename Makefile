@@ -28,19 +28,22 @@ $(BUILD):
 $(BUILD)/scene_build.o: $(CSRC)/scene_build.c $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
+$(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/rtc_render.o $(BUILD)/scene_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so
+$(BUILD)/rtc_frame.o: $(CSRC)/rtc_frame.hip $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/rtc_render.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl
 
 # diagnostic variant (per-wave cycle stamps); never the measured product
 DIAGLIB  := $(LIBDIR)/librtc_diag.so
 $(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -c $< -o $@
 
-$(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/scene_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+$(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -ldl
 
 diag: $(DIAGLIB)
 

@@ -1,24 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s + frame time of the MI355X render path on BASELINE.json's workload.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ultracomplex_1080p64|ultracomplex_4k64]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ultracomplex_1080p64|...]
 
-A step = one frame: every rank renders its interleaved rows (y = rank + k*N, main.c:84 lifted to GPUs) with
-the HIP kernel, the uint8 parts are gathered to rank 0 over RCCL (torch.distributed `nccl`) and re-interleaved
-on rank 0.  The scene (ultracomplex.obj as the reference's loader produced it, tests/golden/scenes) is resident
-in HBM before timing; outputs stay in HBM (the D2H of the finished frame is reported separately).
+A step = one frame, timed as SURVEY.md §8(d) / BASELINE.md §3 define it: from the render launch until the
+frame's Color[W*H] is in host memory (the buffer main.c:305 hands to stbi_write_bmp).  Every rank renders its
+interleaved rows (y = rank + k*N, main.c:84 lifted to GPUs) with the HIP kernels, the uint8 parts are gathered
+to rank 0 over RCCL (torch.distributed `nccl`) and re-interleaved there, and rank 0 copies the frame into pinned
+host memory (hipMemcpyAsync on a copy stream; frame k's copy overlaps frame k+1's render, double-buffered).
+The scene (the reference loader's Triangle[], tests/golden/scenes) is resident in HBM before timing.
 
-Prints ONE JSON line on rank 0.  `value` = W*H*spp*K / t / 1e6 over the whole job (strong scaling: the frame
-is fixed, N GPUs split it).  `roofline` is the dominant (render) kernel against the FP32 VALU peak with the
-survey's algorithmic 57 flop per ray-triangle test (SURVEY.md §8 d); `cpu_baseline` is the CPU restatement
-of the reference (oracle/, "port") on a bounded row sample of the same frame, rank 0 at N = 1 only.
+Prints ONE JSON line on rank 0.  `value` = W*H*spp*K / t / 1e6 over the whole job (strong scaling: the frame is
+fixed, N GPUs split it).  `roofline` is the dominant (heavy-tile) kernel against the FP32 VALU peak with the
+survey's algorithmic 57 flop per ray-triangle test (SURVEY.md §8 d); `cpu_baseline` is the CPU restatement of
+the reference (oracle/, "port") on the same workload on the box's host cores, beside the reference itself
+compiled here (oracle/_ref/rtc_ref), rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -28,12 +34,18 @@ METRIC = "Mrays/sec + frame time, 1920x1080x64spp ultracomplex.obj, 1/2/4/8 GPUs
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (FP32 vector, spec)
 HBM_PEAK_GBS = 8000.0
 FLOPS_PER_TEST = 57  # full rayTriangle path
+# BASELINE.json configs: C1 simplest 256x256x1 (CPU), C2 cube 1080p16, C3 fsuzane 1080p64, C4 complex 4K64,
+# C5 ultracomplex 4K256, NS ultracomplex 4K64; the metric's own config is ultracomplex 1080p64
 WORKLOADS = {
     "ultracomplex_1080p64": ("ultracomplex", 1920, 1080, 64),
     "ultracomplex_4k64": ("ultracomplex", 3840, 2160, 64),
+    "ultracomplex_4k256": ("ultracomplex", 3840, 2160, 256),
+    "complex_4k64": ("complex", 3840, 2160, 64),
     "fsuzane_1080p64": ("fsuzane", 1920, 1080, 64),
     "cube_1080p16": ("cube", 1920, 1080, 16),
+    "simplest_256p1": ("simplest", 256, 256, 1),
 }
+REF_THREADS = 12  # main.c:43 NUMBER_OF_THREADS
 
 
 def load_scene(name):
@@ -46,40 +58,116 @@ def load_scene(name):
     return np.frombuffer(raw[8:8 + 68 * int(count)], TRIANGLE_DT).copy(), int(tonly)
 
 
-def cpu_baseline(tris, tonly, scene, cam, W, H, spp, row_stride):
-    """The reference algorithm on the host (oracle/rtc_oracle.c, bit-identical to the reference on the golden
-    fixtures) over rows y = 0, s, 2s, ... of the same frame.  Threads = the box's CPU share (<= 16)."""
+# ---- CPU baseline --------------------------------------------------------------------------------------
+def cpu_info() -> dict:
+    """lscpu model and topology, nproc, and this process's CPU share (affinity, cgroup quota)."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["nproc"]
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["model"] = kv.get("Model name", "")
+        info["sockets"] = int(kv.get("Socket(s)", "0") or 0)
+        info["cores_per_socket"] = int(kv.get("Core(s) per socket", "0") or 0)
+        info["threads_per_core"] = int(kv.get("Thread(s) per core", "0") or 0)
+    except Exception:
+        pass
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpus"] = None if q == "max" else round(int(q) / int(p), 2)
+    except Exception:
+        info["cgroup_cpus"] = None
+    return info
+
+
+def cpu_baseline(tris, tonly, scene, cam, W, H, spp, budget_samples, gpu_colors, gpu_accum):
+    """The reference algorithm on the host: the CPU restatement (oracle/rtc_oracle.c, bit-identical to the
+    reference on every golden fixture; gcc -O3, no FMA) with row-interleaved pthreads like main.c:84 at
+    threads = nproc and at the reference's 12, plus the reference's own sources compiled here
+    (oracle/_ref/rtc_ref, 12 threads, its own main) when the whole frame fits the budget.  Rows
+    y = 0, s, 2s, ... of the same frame with s = ceil(samples / budget) (s = 1 at the metric's config)."""
+    import hashlib
+
+    import numpy as np
+
     import oracle.binding as orc
+    import raytracingc_amd as rt
     from raytracingc_amd._abi import RtcRenderDesc
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
-    d = RtcRenderDesc(W, H, spp, 10, tonly, 0, row_stride, 0)
-    t0 = time.perf_counter()
-    colors, _, seg = orc.render(tris, None, scene, cam, d, threads=threads)
-    dt = time.perf_counter() - t0
-    rows = colors.shape[0]
+    info = cpu_info()
+    stride = max(1, math.ceil(W * H * spp / budget_samples))
+    d = RtcRenderDesc(W, H, spp, 10, tonly, 0, stride, 0)
+
+    def run(threads):
+        t0 = time.perf_counter()
+        colors, accum, seg = orc.render(tris, None, scene, cam, d, threads=threads)
+        return time.perf_counter() - t0, colors, accum, seg
+
+    n_all = info["nproc"]
+    dt, ccol, cacc, seg = run(n_all)
+    dt12, _, _, _ = run(REF_THREADS)
+    rows = ccol.shape[0]
     samples = rows * W * spp
-    return {
-        "value": samples / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-        "sample": f"rows y=0 mod {row_stride} of the same frame ({rows} rows x {W} x {spp} spp = {samples} samples, "
-                  f"{seg} segments), {dt:.2f} s wall on {threads} threads; oracle/rtc_oracle.c (gcc -O3, no FMA)",
-        "seconds": dt,
-    }, colors
+    res = {
+        "value": samples / dt / 1e6, "unit": "Mrays/s", "cores": n_all, "kind": "port",
+        "threads": n_all, "value_12t": round(samples / dt12 / 1e6, 3),
+        "cpu_model": info.get("model"),
+        "topology": f"{info.get('sockets')} sockets x {info.get('cores_per_socket')} cores x "
+                    f"{info.get('threads_per_core')} SMT = nproc {info['nproc']}; affinity {info['affinity']} CPUs, "
+                    f"cgroup quota {info.get('cgroup_cpus')} CPUs",
+        "sample": (f"{'the whole frame' if stride == 1 else f'rows y = 0 mod {stride} of the frame'} ({rows} rows x "
+                   f"{W} x {spp} spp = {samples} samples, {seg} segments), render loop only: {dt:.2f} s on {n_all} "
+                   f"threads, {dt12:.2f} s on {REF_THREADS}; oracle/rtc_oracle.c (gcc -O3, no FMA)"),
+    }
+    g_rows = gpu_colors[::stride]
+    res["u8_mismatch_vs_gpu"] = int((g_rows != ccol).any(-1).sum())
+    res["float_bits_equal_vs_gpu"] = bool(gpu_accum is not None and
+                                          np.array_equal(gpu_accum[::stride].view(np.uint32), cacc.view(np.uint32)))
+    ref_bin = orc.REF_BIN
+    if os.path.exists(ref_bin) and W * H * spp <= 1.5 * budget_samples:
+        with tempfile.TemporaryDirectory() as tmp:
+            obj = os.path.join(tmp, "scene.obj")
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from obj_export import write_obj  # the fixture as an OBJ + MTL the reference loads byte for byte
+
+            write_obj(obj, tris)
+            bmp = os.path.join(tmp, "ref.bmp")
+            t0 = time.perf_counter()
+            r = subprocess.run([ref_bin, "--spp", str(spp), "-i", obj, "-s", str(W), str(H), "-o", bmp], cwd=tmp,
+                               capture_output=True, text=True, timeout=600)
+            dtr = time.perf_counter() - t0
+            if r.returncode == 0:
+                gbmp = os.path.join(tmp, "gpu.bmp")
+                rt.write_bmp(gbmp, gpu_colors)
+                res["ref_value"] = round(W * H * spp / dtr / 1e6, 3)
+                res["ref_sample"] = (f"the reference's own main (main.c:107-305, sources under /root/reference built by "
+                                     f"`make ref`, deterministic variant oracle/ref_unity.c), whole frame, "
+                                     f"{REF_THREADS} threads, {dtr:.2f} s wall incl. OBJ load and BMP write")
+                res["ref_bmp_equals_gpu_bmp"] = (hashlib.md5(open(bmp, "rb").read()).hexdigest() ==
+                                                 hashlib.md5(open(gbmp, "rb").read()).hexdigest())
+            else:
+                res["ref_error"] = r.stderr[-300:]
+    return res
 
 
+# ---- GPU ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="ultracomplex_1080p64", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-stride", type=int, default=4)
-    ap.add_argument("--no-hoisted", action="store_true", help="skip the extra hoisted-mode measurement")
+    ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
+                    help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
+    ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
     args = ap.parse_args()
 
     import numpy as np
@@ -87,7 +175,7 @@ def main():
     import torch.distributed as dist
 
     import raytracingc_amd as rt
-    from raytracingc_amd.distributed import FrameRenderer, hip_part_renderer
+    from raytracingc_amd.distributed import rank_config, rows_per_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -105,110 +193,129 @@ def main():
     cam = rt.camera_basis()
     ds = rt.DeviceScene(tris, None, device=local)
     seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device=dev)
+    rows = rows_per_rank(H, world)
+    stream = torch.cuda.current_stream(dev)
+    copy_stream = torch.cuda.Stream(dev)
+    part = torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) if world > 1 else None
+    gathered = torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
+    nbuf = 2
+    frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
+    host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
 
-    def make(hoist, tile_cull=True):
-        cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist, tile_cull=tile_cull)
-        return FrameRenderer(cfg, hip_part_renderer(ds, scene, cam, seg), dev)
+    def frame_step(cfg, b, d2h=True, copy_events=None):
+        """One frame into device frame buffer b (rank 0), then its D2H into pinned host buffer b."""
+        cfg_r = rank_config(cfg, rank, world)
+        if world == 1:
+            ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
+        else:
+            ds.render_rows_async(scene, cam, cfg_r, part.data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
+            dist.gather(part, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(), stream.cuda_stream)
+        if rank == 0 and d2h:
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            copy_stream.wait_event(ready)
+            with torch.cuda.stream(copy_stream):
+                if copy_events is not None:
+                    copy_events[0].record(copy_stream)
+                host[b].copy_(frames[b], non_blocking=True)
+                if copy_events is not None:
+                    copy_events[1].record(copy_stream)
+            done = torch.cuda.Event()
+            done.record(copy_stream)
+            return done
+        return None
 
-    def run(fr, steps, warmup):
-        stream = torch.cuda.current_stream(dev)
-        for _ in range(warmup):
-            fr()
-        evs = []
+    def run(cfg, steps, warmup, d2h=True):
+        copied = [None] * nbuf
+        for k in range(warmup):
+            frame_step(cfg, k % nbuf, d2h)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         seg.zero_()
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         t0 = time.perf_counter()
-        for _ in range(steps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            # the render kernel runs first in each step, on this stream: e0..e1 brackets it alone
-            e0.record(stream)
-            fr.render_part(fr.cfg_r, fr.part)
-            e1.record(stream)
-            evs.append((e0, e1))
-            # rest of the step (gather + re-interleave)
-            if world > 1:
-                glist = list(fr.gathered.unbind(0)) if rank == 0 else None
-                dist.gather(fr.part, gather_list=glist, dst=0)
-            elif rank == 0:
-                fr.gathered[0].copy_(fr.part)
-            if rank == 0:
-                rt.deinterleave_async(fr.gathered.data_ptr(), fr.world, fr.rows, W, H, fr.frame.data_ptr(),
-                                      stream.cuda_stream)
+        for k in range(steps):
+            b = k % nbuf
+            if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
+                stream.wait_event(copied[b])
+            copied[b] = frame_step(cfg, b, d2h, cev[k] if (d2h and rank == 0) else None)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        kern_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-        t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         segs = seg.clone()
         if world > 1:
             dist.all_reduce(segs)
-        return float(t[0]), float(t[1]), [int(v) // steps for v in segs.tolist()]
+        d2h_ms = (sum(a.elapsed_time(b) for a, b in cev) / steps) if (d2h and rank == 0) else None
+        return float(t[0]), [int(v) // steps for v in segs.tolist()], d2h_ms
 
-    fr = make(False)
-    t, kern_ms, (seg_calls, seg_traced, tri_tests, cluster_tests) = run(fr, args.steps, args.warmup)
+    cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly))
+    t, (seg_calls, seg_traced, tri_tests, cluster_tests), d2h_ms = run(cfg, args.steps, args.warmup)
     samples = W * H * spp
     value = samples * args.steps / t / 1e6
-    frame = fr.frame.clone() if rank == 0 else None
+    # the last frame of the timed run as it landed in host memory
+    host_frame = host[(args.steps - 1) % nbuf].numpy().copy() if rank == 0 else None
+
     # per-kernel device times of the split launch (HIP events the library records around the heavy-tile
-    # kernel on this stream and around the sky kernel on the scene's side stream), after the timed region:
-    # reading them waits for each launch
+    # kernel on this stream and around the sky kernel on the scene's side stream), after the timed region
     heavy_ms = sky_ms = None
     kt = []
     ds.set_timing(True)
     for _ in range(max(3, min(args.steps, 10))):
-        fr.render_part(fr.cfg_r, fr.part)
+        ds.render_rows_async(scene, cam, rank_config(cfg, rank, world), (part if world > 1 else frames[0]).data_ptr(),
+                             None, None, stream.cuda_stream)
         k = ds.kernel_times()
         if k:
             kt.append(k)
     ds.set_timing(False)
     if kt:
-        heavy_ms = sum(a for a, _ in kt) / len(kt)
-        sky_ms = sum(b for _, b in kt) / len(kt)
-        hk = torch.tensor([heavy_ms, sky_ms], dtype=torch.float64, device=dev)
+        hk = torch.tensor([sum(a for a, _ in kt) / len(kt), sum(b for _, b in kt) / len(kt)], dtype=torch.float64,
+                          device=dev)
         if world > 1:
             dist.all_reduce(hk, op=dist.ReduceOp.MAX)
         heavy_ms, sky_ms = float(hk[0]), float(hk[1])
 
-    hoisted = brute = None
-    if not args.no_hoisted:
-        frh = make(True)
-        th, kh, (hc, ht, htests, _) = run(frh, args.steps, 1)
-        hoisted = {"value": round(samples * args.steps / th / 1e6, 3), "ms_per_step": round(th / args.steps * 1e3, 4),
-                   "kernel_ms": round(kh, 4), "segments_traced": ht, "tri_tests": htests,
-                   "bit_exact_vs_faithful": bool(rank != 0 or torch.equal(frh.frame, frame))}
-        # the same faithful frame without the tile candidate lists (every primary segment tests every
-        # triangle, as calculateRayCollision does): for comparison only
-        frb = make(False, tile_cull=False)
-        tb, kb, (bc, bt, btests, _) = run(frb, max(2, args.steps // 2), 1)
-        brute = {"value": round(samples * max(2, args.steps // 2) / tb / 1e6, 3),
-                 "ms_per_step": round(tb / max(2, args.steps // 2) * 1e3, 4), "kernel_ms": round(kb, 4),
-                 "tri_tests": btests, "bit_exact_vs_culled": bool(rank != 0 or torch.equal(frb.frame, frame))}
+    extras = {}
+    if not args.no_extras:
+        # device-only frames (no D2H), the bit-exact hoisted mode and the brute-force primary segments
+        td, _, _ = run(cfg, args.steps, 1, d2h=False)
+        extras["device_only"] = {"ms_per_step": round(td / args.steps * 1e3, 4),
+                                 "value": round(samples * args.steps / td / 1e6, 3)}
+        ref_frame = frames[0].clone() if rank == 0 else None
+        th, (_, ht, htests, _), _ = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist=True), args.steps, 1)
+        extras["hoisted"] = {"value": round(samples * args.steps / th / 1e6, 3),
+                             "ms_per_step": round(th / args.steps * 1e3, 4), "segments_traced": ht,
+                             "tri_tests": htests,
+                             "bit_exact_vs_faithful": bool(rank != 0 or torch.equal(frames[0], ref_frame))}
+        nb = max(2, args.steps // 4)
+        tb, (_, _, btests, _), _ = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), tile_cull=False), nb, 1)
+        extras["no_tile_cull"] = {"value": round(samples * nb / tb / 1e6, 3), "ms_per_step": round(tb / nb * 1e3, 4),
+                                  "tri_tests": btests}
+        # single-frame latency: render .. Color[] on the host, nothing overlapped
+        if rank == 0 and world == 1:
+            lat = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                ds.render_rows_async(scene, cam, cfg, frames[0].data_ptr(), None, None, stream.cuda_stream)
+                host[0].copy_(frames[0], non_blocking=True)
+                e1.record(stream)
+                e1.synchronize()
+                lat.append(e0.elapsed_time(e1))
+            extras["frame_latency_ms"] = round(sorted(lat)[len(lat) // 2], 4)
 
     if rank == 0:
-        # D2H of the finished frame, reported separately (never `value`)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        host = frame.cpu()
-        d2h_ms = (time.perf_counter() - t0) * 1e3
         T = len(tris)
-        # ray-triangle tests the kernel evaluated per frame, all ranks (device counter: each traced segment x
-        # the triangles it visits -- its tile's candidates for a primary segment, all T otherwise)
-        tests = tri_tests
-        # per launch on one GPU: this rank's share of the tests; kernel time = mean of its launches
-        tests_per_launch = tests / world
-        # the dominant kernel: rtc_render_heavy (every ray-triangle test runs there; the sky kernel tests none)
-        dom_ms = heavy_ms if heavy_ms else kern_ms
+        tests_per_launch = tri_tests / world
+        dom_ms = heavy_ms if heavy_ms else t / args.steps * 1e3
         achieved_tf = tests_per_launch * FLOPS_PER_TEST / (dom_ms * 1e-3) / 1e12
-        # SURVEY §8(d)'s brute-force count (traced segments x T x 57): the work calculateRayCollision does
-        bf_tf = seg_traced / world * T * FLOPS_PER_TEST / (kern_ms * 1e-3) / 1e12
-        scene_bytes = T * 68
-        out_bytes = fr.rows * W * 3
-        alg_bytes = scene_bytes + out_bytes
+        bf_tf = seg_traced / world * T * FLOPS_PER_TEST / (t / args.steps) / 1e12
         traffic = None
         pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
@@ -234,42 +341,39 @@ def main():
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
-                       "mode": "faithful (every sample re-traces its primary ray: primary segments over the 8x8 tile's "
-                            "candidate triangles, bounce segments over the triangle clusters their half-line may reach)"},
+                       "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
+                               "(double-buffered: frame k's D2H overlaps frame k+1's render)",
+                       "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
+                               "environment)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
-                         "kernel": "rtc_render_heavy" if heavy_ms else "rtc_render_kernel",
+                         "kernel": "rtc_render_heavy (heavy-tile kernel of the split launch)",
                          "kernel_ms": round(dom_ms, 4),
                          "sky_kernel_ms": round(sky_ms, 4) if sky_ms else None,
-                         "launch_ms": round(kern_ms, 4),
                          "work_per_launch": f"{tests_per_launch:.4g} ray-triangle tests x {FLOPS_PER_TEST} flop",
                          "cluster_tests_per_launch": cluster_tests // world,
-                         "hbm_achieved_gbs": round(alg_bytes / (dom_ms * 1e-3) / 1e9, 3),
+                         "hbm_achieved_gbs": (round(traffic / (dom_ms * 1e-3) / 1e9, 3) if traffic else None),
                          "hbm_peak_gbs": HBM_PEAK_GBS,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
-                         # SURVEY.md §8(d)'s formula: segments_traced x T x 57 / (t x 157.3e12 x G); above 1
-                         # because the culling layers skip ~99 % of the brute-force tests (bit-exactly)
-                         "survey_formula_frac": round(bf_tf / FP32_VALU_PEAK_TFLOPS, 4),
-                         "note": "achieved: the ray-triangle tests evaluated x 57 flop / the heavy-tile kernel's "
-                                 "device time (HIP events around it); launch_ms: the whole launch sequence (cull, "
-                                 "order, sky || heavy, counters); bruteforce_equiv: segments x T (the reference's "
-                                 "brute-force work) over launch_ms"},
+                         "note": "achieved: the ray-triangle tests the kernel evaluated x 57 flop / its device time "
+                                 "(HIP events around it on the launch stream); traffic: rocprofv3 FETCH_SIZE x 2 + "
+                                 "WRITE_SIZE per launch (profiles/pmc_traffic.json); hbm_achieved_gbs: traffic / "
+                                 "kernel time; bruteforce_equiv: segments x T (the reference's brute-force work) per "
+                                 "frame time"},
             "frame_ms": round(t / args.steps * 1e3, 4),
+            "d2h_ms": round(d2h_ms, 4) if d2h_ms is not None else None,
             "segments_per_frame": seg_calls,
             "segments_traced_per_frame": seg_traced,
             "msegments_per_s": round(seg_traced * args.steps / t / 1e6, 2),
-            "tri_tests_per_frame": tests,
-            "gtests_per_s": round(tests * args.steps / t / 1e9, 2),
-            "d2h_ms": round(d2h_ms, 3),
-            "hoisted": hoisted,
-            "no_tile_cull": brute,
+            "tri_tests_per_frame": tri_tests,
+            "gtests_per_s": round(tri_tests * args.steps / t / 1e9, 2),
         }
+        line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
-            cb, ccol = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_row_stride)
-            gpu_rows = host.numpy()[::args.cpu_row_stride]
-            cb["u8_mismatch_vs_gpu"] = int((gpu_rows != ccol).any(-1).sum())
-            cb.pop("seconds")
+            # the GPU's float frame for the bit comparison (one more render through the C ABI)
+            _, gacc, _ = rt.render(tris, None, scene, cam, cfg, device=local, want_accum=True)
+            cb = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_budget_samples, host_frame, gacc)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(line), flush=True)

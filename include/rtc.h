@@ -11,7 +11,9 @@
  * pass through unconverted.
  *
  * Error convention: 0 = OK; a negative value is either -(hipError_t) (|v| < 10000) or one of the RTC_E*
- * codes below.  Nothing here calls exit(); rtc_last_error() returns a message for the calling thread.
+ * codes below; a positive value is an RCCL ncclResult_t (rtc_render_multi).  Nothing here calls exit();
+ * rtc_last_error() returns a message for the calling thread.  Entry points that select a device restore
+ * the caller's current device before returning.
  */
 #ifndef RTC_H
 #define RTC_H
@@ -74,12 +76,15 @@ typedef struct RtcRenderDesc {
                                      cooperative kernel (lanes split each segment) */
 
 typedef struct RtcStats {
-    double renderMs;             /* device time of the render kernel(s), HIP events */
-    double totalMs;              /* wall time of the whole rtc_render call incl. uploads / D2H */
+    double renderMs;             /* device time of the render launch (slowest device), HIP events */
+    double totalMs;              /* wall time of the whole call incl. scene upload, allocations, readback */
     unsigned long long segments; /* closest-hit queries traced (calculateRayCollision calls) */
     unsigned long long samples;  /* camera samples = pixels * spp */
     unsigned long long triTests; /* ray-triangle tests evaluated (segments x triangles the segment visits) */
     unsigned long long clusterTests; /* ray-cluster bounding-ball tests (cooperative path, bounce rays) */
+    double frameMs;              /* SURVEY.md §8(d) frame time: first render kernel launch after the scene upload
+                                    until Color[W*H] is in (pinned) host memory -- render, RCCL gather and
+                                    re-interleave (multi), D2H; HIP events on device 0 */
 } RtcStats;
 
 /* ---- error codes ----------------------------------------------------------------------------------- */
@@ -122,10 +127,13 @@ int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sp
                const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int device,
                Color *outImage, float *outAccum, RtcStats *stats);
 
-/* Single-process multi-GPU variant of rtc_render: devices 0..numDevices-1 each render the rows
- * y = g + k*numDevices (the reference's row interleave, main.c:84, lifted to GPUs), concurrently; the
- * parts are copied back and re-interleaved.  Output is bit-identical to numDevices = 1 (the seed is the
- * absolute pixel index, main.c:95).  stats->renderMs = slowest device. */
+/* Single-process multi-GPU variant of rtc_render (replaces the 12-pthread fan-out main.c:285-302): devices
+ * 0..numDevices-1 each render the rows y = g + k*numDevices (the reference's row interleave, main.c:84,
+ * lifted to GPUs) into a compact part, concurrently; one RCCL communicator clique (ncclCommInitAll) gathers
+ * the parts to device 0 over xGMI (ncclGather, grouped), device 0 re-interleaves them and one D2H brings the
+ * frame to the host.  Output is bit-identical to numDevices = 1 (the seed is the absolute pixel index,
+ * main.c:95).  RCCL errors are returned as positive ncclResult_t values.  stats->renderMs = slowest
+ * device's render launch; stats->frameMs = render + gather + re-interleave + D2H. */
 int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                      const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
                      Color *outImage, float *outAccum, RtcStats *stats);

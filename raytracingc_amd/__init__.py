@@ -167,6 +167,11 @@ def _arr(a, dt):
     return a, len(a)
 
 
+def _stats(st: RtcStats) -> dict:
+    return {"render_ms": st.renderMs, "frame_ms": st.frameMs, "total_ms": st.totalMs, "segments": st.segments,
+            "samples": st.samples, "tri_tests": st.triTests, "cluster_tests": st.clusterTests}
+
+
 def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, device: int = -1,
            want_accum: bool = False):
     """The render seam (main.c:263-304) on one GPU.  Returns (colors uint8 [rows, W, 3],
@@ -180,9 +185,7 @@ def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, devic
     d = cfg.desc()
     check(lib().rtc_render(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), device,
                            _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render")
-    return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples, "tri_tests": st.triTests,
-                           "cluster_tests": st.clusterTests}
+    return colors, accum, _stats(st)
 
 
 def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, num_devices: int,
@@ -196,9 +199,7 @@ def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig,
     d = cfg.desc()
     check(lib().rtc_render_multi(_ptr(t), nt, _ptr(s), ns, C.byref(scene), C.byref(cam), C.byref(d), num_devices,
                                  _ptr(colors), _ptr(accum), C.byref(st)), "rtc_render_multi")
-    return colors, accum, {"render_ms": st.renderMs, "total_ms": st.totalMs, "segments": st.segments,
-                           "samples": st.samples, "tri_tests": st.triTests,
-                           "cluster_tests": st.clusterTests}
+    return colors, accum, _stats(st)
 
 
 class DeviceScene:

@@ -72,6 +72,7 @@ class RtcStats(C.Structure):
         ("samples", C.c_ulonglong),
         ("triTests", C.c_ulonglong),
         ("clusterTests", C.c_ulonglong),
+        ("frameMs", C.c_double),
     ]
 
 

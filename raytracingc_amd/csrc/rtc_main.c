@@ -159,8 +159,8 @@ int main(int argc, char const *argv[])
         return 2;
     }
     if (stats)
-        printf("render %.3f ms, %.1f Mrays/s, %llu segments\n", st.renderMs,
-               st.renderMs > 0 ? (double)st.samples / (st.renderMs * 1e3) : 0.0, st.segments);
+        printf("frame %.3f ms (render %.3f ms), %.1f Mrays/s, %llu segments\n", st.frameMs, st.renderMs,
+               st.frameMs > 0 ? (double)st.samples / (st.frameMs * 1e3) : 0.0, st.segments);
     if (rtc_write_bmp(out, width, height, image) != 0)
         fprintf(stderr, "%s\n", rtc_last_error());
     if (dumpFloat) {

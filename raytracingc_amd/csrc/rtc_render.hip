@@ -29,6 +29,7 @@
 #include "../../include/rtc.h"
 #include "rtc_device.h"
 #include "rtc_internal.h"
+#include "rtc_hip_util.h"
 
 static_assert(sizeof(vec3) == 12, "vec3 layout");
 static_assert(sizeof(Material) == 20, "Material layout");
@@ -66,13 +67,6 @@ extern "C" void rtc_log(int level, const char *fmt, ...)
 extern "C" const char *rtc_last_error(void) { return g_err; }
 extern "C" const char *rtc_version(void) { return "rtc-mi355x 0.1 (gfx950)"; }
 
-#define HIP_TRY(expr)                                                                                  \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess)                                                                          \
-            return rtc_fail(-(int)e_, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
-                            __LINE__);                                                                 \
-    } while (0)
 
 extern "C" int rtc_device_count(int *count)
 {
@@ -344,7 +338,9 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         HIP_TRY(hipGetDevice(&device));
     if (device >= n)
         return rtc_fail(RTC_EINVAL, "device %d out of range (%d devices)", device, n);
-    HIP_TRY(hipSetDevice(device));
+    RtcDeviceGuard guard(device);
+    if (!guard.ok())
+        return rtc_fail(RTC_ENODEV, "rtc_scene_upload: cannot select device %d", device);
     std::vector<DevTri> dt;
     std::vector<DevMat> dm;
     std::vector<DevSphere> ds;
@@ -2543,6 +2539,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const int rows = rtc_rows_selected(d);
     if (rows == 0)
         return 0;
+    /* the scene's buffers, scratch and kernels live on s->device; the caller's current device is restored */
+    RtcDeviceGuard guard(s->device);
+    if (!guard.ok())
+        return rtc_fail(RTC_ENODEV, "rtc_render_rows_async: cannot select the scene's device %d", s->device);
     RenderParams P;
     memset(&P, 0, sizeof P);
     P.tris = s->tris;
@@ -2719,203 +2719,6 @@ extern "C" int rtc_deinterleave_async(const void *dCompact, int parts, int rowsP
     hipLaunchKernelGGL(rtc_deinterleave_kernel, grid, dim3(256), 0, (hipStream_t)stream,
                        (const unsigned char *)dCompact, parts, rowsPerPart, rowBytes, height, (unsigned char *)dOut);
     HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-/* ---- host-buffer render (the main.c:263-304 seam) ------------------------------------------------- */
-template <typename T> struct DevBuf {
-    T *p = nullptr;
-    ~DevBuf()
-    {
-        if (p)
-            (void)hipFree(p);
-    }
-};
-
-constexpr size_t kSegBytes = RTC_SEGMENT_COUNTERS * sizeof(unsigned long long);
-
-extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
-                          const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int device,
-                          Color *outImage, float *outAccum, RtcStats *stats)
-{
-    auto t0 = std::chrono::steady_clock::now();
-    if (!scene || !cam || !d || !outImage)
-        return rtc_fail(RTC_EINVAL, "rtc_render: null argument");
-    RtcDeviceScene *s = nullptr;
-    int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, device, &s);
-    if (rc)
-        return rc;
-    struct Guard {
-        RtcDeviceScene *s;
-        ~Guard() { rtc_scene_release(s); }
-    } guard{s};
-    const int rows = rtc_rows_selected(d);
-    const size_t px = (size_t)rows * (size_t)(d->width > 0 ? d->width : 0);
-    DevBuf<unsigned char> dColors;
-    DevBuf<float> dAccum;
-    DevBuf<unsigned long long> dSeg;
-    HIP_TRY(hipMalloc(&dColors.p, px * 3 + 16));
-    if (outAccum)
-        HIP_TRY(hipMalloc(&dAccum.p, px * 3 * sizeof(float) + 16));
-    HIP_TRY(hipMalloc(&dSeg.p, kSegBytes));
-    HIP_TRY(hipMemset(dSeg.p, 0, kSegBytes));
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, nullptr));
-    rc = rtc_render_rows_async(s, scene, cam, d, dColors.p, dAccum.p, dSeg.p, nullptr);
-    if (rc) {
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        return rc;
-    }
-    HIP_TRY(hipEventRecord(e1, nullptr));
-    HIP_TRY(hipEventSynchronize(e1));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    HIP_TRY(hipMemcpy(outImage, dColors.p, px * 3, hipMemcpyDeviceToHost));
-    if (outAccum)
-        HIP_TRY(hipMemcpy(outAccum, dAccum.p, px * 3 * sizeof(float), hipMemcpyDeviceToHost));
-    unsigned long long seg[RTC_SEGMENT_COUNTERS] = {0};
-    HIP_TRY(hipMemcpy(seg, dSeg.p, kSegBytes, hipMemcpyDeviceToHost));
-    if (stats) {
-        stats->renderMs = ms;
-        stats->segments = seg[0];
-        stats->samples = (unsigned long long)px * (unsigned long long)(d->spp > 0 ? d->spp : 0);
-        stats->triTests = seg[2];
-        stats->clusterTests = seg[3];
-        stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
-    return 0;
-}
-
-extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
-                                const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
-                                Color *outImage, float *outAccum, RtcStats *stats)
-{
-    auto t0 = std::chrono::steady_clock::now();
-    if (!scene || !cam || !d || !outImage || numDevices <= 0 || d->rowStart != 0 || d->rowStride != 1)
-        return rtc_fail(RTC_EINVAL, "rtc_render_multi: bad argument (full frames only)");
-    int n = 0;
-    if (int rc = rtc_device_count(&n))
-        return rc;
-    if (numDevices > n)
-        return rtc_fail(RTC_EINVAL, "rtc_render_multi: %d devices requested, %d present", numDevices, n);
-    struct Part {
-        RtcDeviceScene *s = nullptr;
-        unsigned char *col = nullptr;
-        float *acc = nullptr;
-        unsigned long long *seg = nullptr;
-        hipStream_t st = nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        int rows = 0;
-    };
-    std::vector<Part> parts(numDevices);
-    auto cleanup = [&]() {
-        for (int g = 0; g < numDevices; ++g) {
-            Part &p = parts[g];
-            (void)hipSetDevice(g);
-            if (p.col)
-                (void)hipFree(p.col);
-            if (p.acc)
-                (void)hipFree(p.acc);
-            if (p.seg)
-                (void)hipFree(p.seg);
-            if (p.e0)
-                (void)hipEventDestroy(p.e0);
-            if (p.e1)
-                (void)hipEventDestroy(p.e1);
-            if (p.st)
-                (void)hipStreamDestroy(p.st);
-            rtc_scene_release(p.s);
-        }
-    };
-    int rc = 0;
-    for (int g = 0; g < numDevices && !rc; ++g) {
-        Part &p = parts[g];
-        RtcRenderDesc dg = *d;
-        dg.rowStart = g;
-        dg.rowStride = numDevices;
-        p.rows = rtc_rows_selected(&dg);
-        rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s);
-        if (rc)
-            break;
-        const size_t px = (size_t)p.rows * (size_t)d->width;
-        hipError_t e = hipStreamCreate(&p.st);
-        if (e == hipSuccess)
-            e = hipMalloc(&p.col, px * 3 + 16);
-        if (e == hipSuccess && outAccum)
-            e = hipMalloc(&p.acc, px * 3 * sizeof(float) + 16);
-        if (e == hipSuccess)
-            e = hipMalloc(&p.seg, kSegBytes);
-        if (e == hipSuccess)
-            e = hipMemsetAsync(p.seg, 0, kSegBytes, p.st);
-        if (e == hipSuccess)
-            e = hipEventCreate(&p.e0);
-        if (e == hipSuccess)
-            e = hipEventCreate(&p.e1);
-        if (e == hipSuccess)
-            e = hipEventRecord(p.e0, p.st);
-        if (e != hipSuccess) {
-            rc = rtc_fail(-(int)e, "rtc_render_multi setup on device %d: %s", g, hipGetErrorString(e));
-            break;
-        }
-        rc = rtc_render_rows_async(p.s, scene, cam, &dg, p.col, p.acc, p.seg, p.st);
-        if (!rc && (e = hipEventRecord(p.e1, p.st)) != hipSuccess)
-            rc = rtc_fail(-(int)e, "event record: %s", hipGetErrorString(e));
-    }
-    double maxMs = 0;
-    unsigned long long segs = 0, tests = 0, clusterTests = 0;
-    std::vector<unsigned char> col;
-    std::vector<float> acc;
-    for (int g = 0; g < numDevices && !rc; ++g) {
-        Part &p = parts[g];
-        (void)hipSetDevice(g);
-        hipError_t e = hipEventSynchronize(p.e1);
-        float ms = 0;
-        if (e == hipSuccess)
-            e = hipEventElapsedTime(&ms, p.e0, p.e1);
-        const size_t px = (size_t)p.rows * (size_t)d->width;
-        col.resize(px * 3 + 1);
-        unsigned long long sg[RTC_SEGMENT_COUNTERS] = {0};
-        if (e == hipSuccess)
-            e = hipMemcpy(col.data(), p.col, px * 3, hipMemcpyDeviceToHost);
-        if (e == hipSuccess)
-            e = hipMemcpy(sg, p.seg, kSegBytes, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && outAccum) {
-            acc.resize(px * 3 + 1);
-            e = hipMemcpy(acc.data(), p.acc, px * 3 * sizeof(float), hipMemcpyDeviceToHost);
-        }
-        if (e != hipSuccess) {
-            rc = rtc_fail(-(int)e, "rtc_render_multi readback from device %d: %s", g, hipGetErrorString(e));
-            break;
-        }
-        if (ms > maxMs)
-            maxMs = ms;
-        segs += sg[0];
-        tests += sg[2];
-        clusterTests += sg[3];
-        const size_t rowB = (size_t)d->width * 3;
-        for (int k = 0; k < p.rows; ++k) {
-            const int y = g + k * numDevices;
-            memcpy((unsigned char *)outImage + (size_t)y * rowB, col.data() + (size_t)k * rowB, rowB);
-            if (outAccum)
-                memcpy(outAccum + (size_t)y * rowB, acc.data() + (size_t)k * rowB, rowB * sizeof(float));
-        }
-    }
-    cleanup();
-    if (rc)
-        return rc;
-    if (stats) {
-        stats->renderMs = maxMs;
-        stats->segments = segs;
-        stats->samples = (unsigned long long)d->width * d->height * (unsigned long long)(d->spp > 0 ? d->spp : 0);
-        stats->triTests = tests;
-        stats->clusterTests = clusterTests;
-        stats->totalMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
     return 0;
 }
 
@@ -3200,6 +3003,7 @@ extern "C" int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2])
     out[0] = out[1] = -1.f;
     if (!s->timed)
         return 0;
+    RtcDeviceGuard guard(s->device);
     HIP_TRY(hipEventSynchronize(s->evHeavy1));
     HIP_TRY(hipEventSynchronize(s->evSky1));
     HIP_TRY(hipEventElapsedTime(&out[0], s->evHeavy0, s->evHeavy1));

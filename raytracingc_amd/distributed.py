@@ -46,6 +46,8 @@ class FrameRenderer:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # global rank of the group's rank 0, the gather's destination
+        self.root = dist.get_global_rank(group, 0) if (dist.is_initialized() and group is not None) else 0
         self.device = device
         self.rows = rows_per_rank(cfg.height, self.world)
         self.cfg_r = rank_config(cfg, self.rank, self.world)
@@ -61,7 +63,8 @@ class FrameRenderer:
         self.render_part(self.cfg_r, self.part)
         if self.world > 1:
             glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
-            dist.gather(self.part, gather_list=glist, dst=0, group=self.group)
+            # dst is a global rank: the group's rank 0 (dst=0 broke groups without global rank 0)
+            dist.gather(self.part, gather_list=glist, dst=self.root, group=self.group)
         elif self.rank == 0:
             self.gathered[0].copy_(self.part)
         if self.rank != 0:

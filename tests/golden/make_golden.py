@@ -44,7 +44,7 @@ REF_BIN = os.path.join(REPO, "oracle", "_ref", "rtc_ref")
 # scenes used by the BASELINE configs plus loader-quirk scenes (quads: suze; missing mtllib: simple;
 # several materials: rsuzanne, withtexture; mixed: 4geoms)
 OBJ_SCENES = ["simplest", "cube", "fsuzane", "complex", "ultracomplex", "rsuzanne", "suze", "4geoms", "simple",
-              "withtexture"]
+              "withtexture", "suzannes", "asuzane", "plane", "cplane", "fcube", "ccube"]
 
 KAT_KEYS = {}
 
@@ -307,6 +307,15 @@ RENDER_CONFIGS += [
     ("suze_quads_64x36x4", "suze", 64, 36, 4, []),
     ("4geoms_64x36x4", "4geoms", 64, 36, 4, []),
     ("withtexture_64x36x4", "withtexture", 64, 36, 4, []),
+    # the remaining reference models: suzannes.obj (5,208 triangles, the largest, > 256 = the general kernel),
+    # asuzane, plane, cplane, fcube, ccube
+    ("suzannes_96x54x4", "suzannes", 96, 54, 4, []),
+    ("suzannes_cam_64x48x2", "suzannes", 64, 48, 2, ["-p", "-3", "-1", "-3", "-t", "0", "-0.5", "0", "-b", "3"]),
+    ("asuzane_64x36x4", "asuzane", 64, 36, 4, []),
+    ("plane_64x36x4", "plane", 64, 36, 4, []),
+    ("cplane_64x36x4", "cplane", 64, 36, 4, []),
+    ("fcube_64x36x4", "fcube", 64, 36, 4, []),
+    ("ccube_64x36x4", "ccube", 64, 36, 4, []),
 ]
 
 
@@ -362,6 +371,36 @@ def gen_renders(work):
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def gen_meta():
+    """Where the fixtures came from: the glibc whose libm the reference called (powf/log/cos) and the CPU
+    features that decide glibc's ifunc choice (x86-64 powf/log/cos pick their FMA builds when the CPU has
+    FMA + AVX2; rtc_math.h restates the FMA build of powf)."""
+    import platform
+
+    flags = set()
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags") and not flags:
+                flags = set(line.split(":", 1)[1].split())
+            if line.startswith("model name") and not model:
+                model = line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    meta = {
+        "glibc": platform.libc_ver()[1],
+        "cpu_model": model,
+        "cpu_fma": "fma" in flags,
+        "cpu_avx2": "avx2" in flags,
+        "libm_ifunc": "FMA builds of powf/log/cos (fma+avx2 present)" if {"fma", "avx2"} <= flags
+                      else "generic SSE2 builds (no fma/avx2): the device powf restates the FMA build",
+        "compiler": subprocess.run(["gcc", "--version"], capture_output=True, text=True).stdout.splitlines()[0],
+        "ref_binary": "oracle/_ref/rtc_ref (make ref: gcc -O3 on /root/reference sources via oracle/ref_unity.c)",
+    }
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.exists(REF_BIN):
         sys.exit(f"{REF_BIN} missing: run `make ref` (needs {REF_DIR})")
@@ -379,6 +418,7 @@ def main():
         for s in ["ultracomplex", "default"]:
             gen_kat_calc(work, rng, s, debug=True)
         gen_renders(work)
+        gen_meta()
 
 
 if __name__ == "__main__":

@@ -73,6 +73,48 @@ def test_gloo_frame_equals_single_process(world):
     assert np.array_equal(frame, full.numpy())
 
 
+def _subgroup_worker(rank, world, port, q):
+    """Ranks 1..world-1 form a group that excludes global rank 0; the group's rank 0 (global rank 1) must
+    receive the frame (the gather used dst=0, a global rank outside the group)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import raytracingc_amd as rt
+
+        group = dist.new_group(list(range(1, world)))
+        if rank >= 1:
+            cfg = rt.RenderConfig(W, H, SPP, 10, True)
+            fr = FrameRenderer(cfg, _oracle_part, torch.device("cpu"), group=group)
+            assert fr.world == world - 1 and fr.root == 1
+            frame = fr()
+            if rank == 1:
+                q.put(frame.numpy().copy())
+            else:
+                assert frame is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_subgroup_without_global_rank0():
+    import raytracingc_amd as rt
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = torch.zeros((H, W, 3), dtype=torch.uint8)
+    _oracle_part(rt.RenderConfig(W, H, SPP, 10, True), full)
+    assert np.array_equal(frame, full.numpy())
+
+
 def test_partition_helpers():
     import raytracingc_amd as rt
 

@@ -92,6 +92,12 @@ def _render_both(g, hoist=False):
     return col, acc, st, ocol, oacc, oseg
 
 
+# Height-1 frames: H/2 = 0, so every primary direction is NaN (main.c:88-89 divides by (float)(H/2)).  Their
+# floats are NaN on both sides but the NaN sign bit differs (x86 vs gfx950 canonicalisation); the uint8
+# frame and the BMP are identical.  Every other configuration is bit-identical to the reference.
+NAN_SIGN_ONLY = {"complex_1x1x5", "cube_7x1x2"}
+
+
 @pytest.mark.parametrize("name", sorted(GOLD))
 def test_render_matches_oracle(name, gpu_available):
     g = GOLD[name]
@@ -102,7 +108,19 @@ def test_render_matches_oracle(name, gpu_available):
     print(f"{name}: max|d|={mx:.3g} over={over} exact={exact:.5f} u8_mismatch={u8} bit_exact_vs_ref={same_as_reference}")
     assert over == 0 and mx <= TOL
     assert st["segments"] == oseg  # identical paths
-    assert u8 <= max(1, col.shape[0] * col.shape[1] // 1000)
+    assert u8 == 0
+    if name in NAN_SIGN_ONLY:
+        assert np.isnan(acc).all() and np.isnan(oacc).all()
+    else:
+        # the pre-quantisation framebuffer hashes to the reference's own (rtc_ref, tests/golden/make_golden.py)
+        assert same_as_reference
+    # the BMP written from the GPU frame is the reference's, byte for byte
+    bmp = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"rtc_{os.getpid()}_{name}.bmp")
+    rt.write_bmp(bmp, col)
+    try:
+        assert hashlib.md5(open(bmp, "rb").read()).hexdigest() == g["bmp_md5"]
+    finally:
+        os.remove(bmp)
 
 
 @pytest.mark.parametrize("name", ["default_160x90x4", "ultracomplex_160x90x4", "fsuzane_odd_33x17x3",
@@ -315,13 +333,57 @@ def test_spp_not_multiple_of_64(variant, gpu_available):
     assert st["segments"] == oseg
 
 
-def test_render_multi_single_device_equals_render(gpu_available):
-    tris, tonly = load_tris("complex")
+@pytest.mark.parametrize("name", ["complex", "ultracomplex"])
+def test_render_multi_rccl_equals_render(name, gpu_available):
+    """rtc_render_multi over every visible device (ncclCommInitAll clique, ncclGather to device 0, re-interleave,
+    one D2H) == rtc_render bit for bit, colors and floats; the frame time covers the frame's arrival on the
+    host.  On a one-GPU box this runs the whole RCCL path with a clique of one."""
+    tris, tonly = load_tris(name)
     scene, cam, _ = setup_from_flags({})
-    cfg = rt.RenderConfig(64, 48, 4, 10, True)
-    a, fa, _ = rt.render(tris, None, scene, cam, cfg, want_accum=True)
-    b, fb, _ = rt.render_multi(tris, None, scene, cam, cfg, 1, want_accum=True)
+    cfg = rt.RenderConfig(160, 90, 8, 10, True)
+    a, fa, sa = rt.render(tris, None, scene, cam, cfg, want_accum=True)
+    b, fb, sb = rt.render_multi(tris, None, scene, cam, cfg, rt.device_count(), want_accum=True)
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
+    assert sa["segments"] == sb["segments"]
+    assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
+    assert 0 < sa["render_ms"] <= sa["frame_ms"] <= sa["total_ms"]
+
+
+def test_entry_points_restore_current_device(gpu_available):
+    """rtc_render(device=k), rtc_render_multi and a device-resident launch leave the caller's (and torch's)
+    current device where it was (the library used to leave the render's device current)."""
+    import torch
+
+    tris, _ = load_tris("complex")
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(32, 18, 2, 10, True)
+    last = rt.device_count() - 1
+    torch.cuda.set_device(last)
+    rt.render(tris, None, scene, cam, cfg, device=0)
+    assert torch.cuda.current_device() == last
+    rt.render_multi(tris, None, scene, cam, cfg, rt.device_count())
+    assert torch.cuda.current_device() == last
+    ds = rt.DeviceScene(tris, None, device=0)
+    assert torch.cuda.current_device() == last
+    out = torch.zeros((18, 32, 3), dtype=torch.uint8, device="cuda:0")
+    ds.render_rows_async(scene, cam, cfg, out.data_ptr(), stream=torch.cuda.current_stream(0).cuda_stream)
+    torch.cuda.synchronize(0)
+    assert torch.cuda.current_device() == last
+    ds.close()
+    torch.cuda.set_device(0)
+
+
+def test_cli_multi_gpu_flag_uses_rccl_path(tmp_path, gpu_available):
+    """The drop-in CLI's --gpus N (rtc_render_multi, RCCL) writes the reference's BMP byte for byte."""
+    g = GOLD["ultracomplex_160x90x4"]
+    tris, _ = load_tris("ultracomplex")
+    obj = tmp_path / "scene.obj"
+    _write_obj_from_tris(obj, tris)
+    r = subprocess.run([rt.CLI_PATH, "-i", str(obj), "-s", "160", "90", "--spp", "4", "--gpus",
+                        str(rt.device_count()), "--stats", "-o", str(tmp_path / "o.bmp")], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert hashlib.md5((tmp_path / "o.bmp").read_bytes()).hexdigest() == g["bmp_md5"]
 
 
 def test_full_size_properties(gpu_available):
@@ -346,6 +408,44 @@ def test_full_size_properties(gpu_available):
     assert over == 0
 
 
+@pytest.mark.parametrize("scene,W,H,spp,row0,stride", [("cube", 1920, 1080, 16, 3, 24),
+                                                        ("fsuzane", 1920, 1080, 64, 7, 40)])
+def test_full_size_baseline_configs(scene, W, H, spp, row0, stride, gpu_available):
+    """BASELINE.json C2 (cube.obj 1920x1080x16) and C3 (fsuzane.obj 1920x1080x64) at full size on one GPU:
+    deterministic, and a row sample (rows y = row0 + k*stride) matches the oracle bit for bit with identical
+    paths."""
+    tris, tonly = load_tris(scene)
+    sc, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(W, H, spp, 10, True)
+    c1, a1, s1 = rt.render(tris, None, sc, cam, cfg, want_accum=True)
+    c2, a2, s2 = rt.render(tris, None, sc, cam, cfg, want_accum=True)
+    assert np.array_equal(_bits(a1), _bits(a2)) and s1["segments"] == s2["segments"]
+    d = RtcRenderDesc(W, H, spp, 10, tonly, row0, stride, 0)
+    ocol, oacc, oseg = orc.render(tris, None, sc, cam, d, threads=16)
+    assert np.array_equal(_bits(a1[row0::stride]), _bits(oacc)) and np.array_equal(c1[row0::stride], ocol)
+    # the same rows rendered alone on the GPU take the same paths as on the CPU
+    cr, ar, sr = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True, row_start=row0, row_stride=stride),
+                           want_accum=True)
+    assert np.array_equal(_bits(ar), _bits(oacc)) and sr["segments"] == oseg
+    print(f"{scene} {W}x{H}x{spp}: frame {s1['frame_ms']:.3f} ms (render {s1['render_ms']:.3f} ms)")
+
+
+@pytest.mark.parametrize("name", ["suzannes_96x54x4", "suzannes_cam_64x48x2"])
+def test_large_scene_general_kernel(name, gpu_available):
+    """suzannes.obj (5,208 triangles, T > 256: the general kernel) against the reference's golden hash, and
+    tile culling == brute force on it."""
+    g = GOLD[name]
+    tris, tonly = load_tris(g["scene"])
+    assert len(tris) > 256
+    scene, cam, mb = setup_from_flags(g["flags"])
+    base = rt.RenderConfig(g["width"], g["height"], g["spp"], mb, bool(tonly))
+    c1, a1, s1 = rt.render(tris, None, scene, cam, base, want_accum=True)
+    assert hashlib.sha256(a1.tobytes()).hexdigest() == g["float_sha256"]
+    c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**base.__dict__, "tile_cull": False}),
+                           want_accum=True)
+    assert np.array_equal(_bits(a0), _bits(a1)) and s0["segments"] == s1["segments"]
+
+
 def test_edge_sizes(gpu_available):
     tris, tonly = load_tris("fsuzane")
     scene, cam, _ = setup_from_flags({})
@@ -357,14 +457,13 @@ def test_edge_sizes(gpu_available):
 
 
 def _write_obj_from_tris(path, tris):
-    """An OBJ whose loadOBJTriangles result is `tris` (geometry/normals only; default material)."""
-    with open(path, "w") as f:
-        for t in tris:
-            for v in ("posA", "posB", "posC"):
-                f.write(f"v {-t[v]['x']:.9g} {-t[v]['y']:.9g} {t[v]['z']:.9g}\n")
-            f.write(f"vn {-t['normal']['x']:.9g} {-t['normal']['y']:.9g} {t['normal']['z']:.9g}\n")
-        for i in range(len(tris)):
-            f.write(f"f {3 * i + 1}/1/{i + 1} {3 * i + 2}/1/{i + 1} {3 * i + 3}/1/{i + 1}\n")
+    """An OBJ (+ MTL) whose loadOBJTriangles result is `tris` byte for byte (tools/obj_export.py)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from obj_export import write_obj
+
+    write_obj(str(path), tris)
 
 
 @pytest.mark.parametrize("name", ["cube_64x36x4", "C1_simplest_256x256x1"])
