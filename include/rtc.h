@@ -61,19 +61,20 @@ typedef struct RtcRenderDesc {
                                     does) instead of the 8x8 tile's candidate list; same output bit for bit */
 #define RTC_F_NO_REORDER    0x8  /* dispatch workgroups in raster order instead of heaviest first (for A/B
                                     timing; the frame is identical) */
-#define RTC_F_NO_COOP       0x10 /* tiles that see geometry keep one lane per pixel instead of a workgroup
-                                    with 4 cooperating lanes per pixel (A/B timing; the frame is identical) */
-#define RTC_F_NO_CLUSTER_CULL 0x20 /* bounce rays of the cooperative path test every triangle instead of only
-                                      the clusters their half-line may reach (A/B timing; identical frame) */
-#define RTC_F_COOP4         0x40 /* force 4 cooperating lanes per pixel (default: 8 for launches of at most
-                                    700k pixels, else 4; identical frame) */
-#define RTC_F_COOP8         0x80 /* force 8 cooperating lanes per pixel (identical frame) */
-#define RTC_F_PIPE          0x200 /* force the two-samples-in-flight kernel for tiles with geometry (default for
-                                     faithful launches of at most 1.1M pixels; identical frame) */
-#define RTC_F_NO_PIPE       0x400 /* never use it */
-#define RTC_F_SPEC          0x100 /* tiles with geometry: the sample-parallel speculative kernel (lanes = samples,
-                                     RNG states jumped ahead and verified; identical frame) instead of the
-                                     cooperative kernel (lanes split each segment) */
+#define RTC_F_NO_COOP       0x10 /* tiles that see geometry are rendered like the rest, one lane per pixel
+                                    (rtc_render_kernel), instead of by the split launch's heavy-tile kernel
+                                    (A/B timing; the frame is identical) */
+#define RTC_F_NO_CLUSTER_CULL 0x20 /* bounce rays test every triangle instead of only the clusters their
+                                      half-line may reach (A/B timing; identical frame) */
+/* The split launch's heavy-tile kernel is rtc_render_chain (state-indexed samples: lanes evaluate the samples
+ * that start at consecutive RNG offsets, then the chain of the reference's samples is walked in order).  At
+ * most one of the next four flags selects an older kernel instead, for A/B timing (identical frame); two of
+ * them together are RTC_EINVAL. */
+#define RTC_F_COOP4         0x40 /* cooperative kernel, 4 lanes per pixel split each segment */
+#define RTC_F_COOP8         0x80 /* cooperative kernel, 8 lanes per pixel */
+#define RTC_F_PIPE          0x200 /* two samples in flight per pixel (faithful launches only: with
+                                     RTC_F_HOIST_PRIMARY it is RTC_EINVAL) */
+#define RTC_F_SPEC          0x100 /* sample-parallel speculation verified in sample order (lanes = samples) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render launch (slowest device), HIP events */
@@ -82,6 +83,7 @@ typedef struct RtcStats {
     unsigned long long samples;  /* camera samples = pixels * spp */
     unsigned long long triTests; /* ray-triangle tests evaluated (segments x triangles the segment visits) */
     unsigned long long clusterTests; /* ray-cluster bounding-ball tests (cooperative path, bounce rays) */
+    unsigned long long discardedTests; /* ray-triangle tests of speculative samples not accumulated */
     double frameMs;              /* SURVEY.md §8(d) frame time: first render kernel launch after the scene upload
                                     until Color[W*H] is in (pinned) host memory -- render, RCCL gather and
                                     re-interleave (multi), D2H; HIP events on device 0 */
@@ -149,10 +151,12 @@ int rtc_rows_selected(const RtcRenderDesc *d);
  * rows_selected*width*3 bytes; dAccum: nullable device float buffer rows_selected*width*3; dSegments:
  * nullable device u64[RTC_SEGMENT_COUNTERS] the kernel atomically adds to: [0] calculateRayCollision calls
  * (the reference's segment count), [1] closest-hit queries actually traced (smaller with
- * RTC_F_HOIST_PRIMARY), [2] ray-triangle tests evaluated, [3] ray-cluster bounding-ball tests.
+ * RTC_F_HOIST_PRIMARY), [2] ray-triangle tests of the accumulated samples, [3] ray-cluster bounding-ball
+ * tests, [4] ray-triangle tests of speculatively evaluated samples that were not accumulated (state-indexed
+ * window lanes off the chain, mispredicted speculative samples); [2] + [4] = every test evaluated.
  * A scene handle serves one stream at a time: its per-launch scratch (primary-ray records, tile candidate
  * lists) is rewritten by every launch. */
-#define RTC_SEGMENT_COUNTERS 4
+#define RTC_SEGMENT_COUNTERS 5
 /* Per-kernel timing of the split launch: with rtc_scene_set_timing(s, 1) every later launch on s records HIP
  * events around its two kernels (off by default: the records cost each launch a few microseconds), and
  * rtc_scene_kernel_times returns the device times (ms) of the last launch: out[0] the heavy-tile kernel,

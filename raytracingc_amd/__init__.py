@@ -30,7 +30,6 @@ from ._abi import (  # noqa: F401
     RTC_F_COOP8,
     RTC_F_NO_CLUSTER_CULL,
     RTC_F_NO_COOP,
-    RTC_F_NO_PIPE,
     RTC_F_PIPE,
     RTC_F_SPEC,
     RTC_F_NO_REORDER,
@@ -139,17 +138,17 @@ class RenderConfig:
     reorder: bool = True  # dispatch the workgroups that see geometry first (same frame)
     coop: bool = True  # tiles that see geometry: 4 cooperating lanes per pixel (same frame)
     cluster_cull: bool = True  # bounce rays skip triangle clusters they provably miss (same frame)
-    coop_lanes: int = 0  # cooperating lanes per pixel in heavy tiles: 0 = by launch size, 4 or 8 (same frame)
-    spec: bool = False  # heavy tiles: sample-parallel speculative kernel instead of the cooperative one (same frame)
-    pipe: int = 0  # two samples in flight per pixel: 0 = by launch size, 1 = force, -1 = never (same frame)
+    # heavy tiles: rtc_render_chain (state-indexed samples) unless one older kernel is chosen (same frame):
+    coop_lanes: int = 0  # 4 or 8: the cooperative kernel with that many lanes per pixel
+    spec: bool = False  # the sample-parallel speculative kernel
+    pipe: bool = False  # two samples in flight per pixel (faithful only)
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
                 | (RTC_F_COOP4 if self.coop_lanes == 4 else 0) | (RTC_F_COOP8 if self.coop_lanes == 8 else 0)
-                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe > 0 else 0)
-                | (RTC_F_NO_PIPE if self.pipe < 0 else 0))
+                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
@@ -169,7 +168,8 @@ def _arr(a, dt):
 
 def _stats(st: RtcStats) -> dict:
     return {"render_ms": st.renderMs, "frame_ms": st.frameMs, "total_ms": st.totalMs, "segments": st.segments,
-            "samples": st.samples, "tri_tests": st.triTests, "cluster_tests": st.clusterTests}
+            "samples": st.samples, "tri_tests": st.triTests, "cluster_tests": st.clusterTests,
+            "discarded_tests": st.discardedTests}
 
 
 def render(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig, device: int = -1,

@@ -72,6 +72,7 @@ class RtcStats(C.Structure):
         ("samples", C.c_ulonglong),
         ("triTests", C.c_ulonglong),
         ("clusterTests", C.c_ulonglong),
+        ("discardedTests", C.c_ulonglong),
         ("frameMs", C.c_double),
     ]
 
@@ -86,8 +87,7 @@ RTC_F_COOP4 = 0x40
 RTC_F_COOP8 = 0x80
 RTC_F_SPEC = 0x100
 RTC_F_PIPE = 0x200
-RTC_F_NO_PIPE = 0x400
-RTC_SEGMENT_COUNTERS = 4  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
+RTC_SEGMENT_COUNTERS = 5  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
 assert C.sizeof(Vec3) == 12 and C.sizeof(Scene) == 56 and C.sizeof(Material) == 20

@@ -130,6 +130,7 @@ void fill_stats(RtcStats *stats, double renderMs, double frameMs, const unsigned
     stats->samples = (unsigned long long)pixels * (unsigned long long)(d->spp > 0 ? d->spp : 0);
     stats->triTests = seg[2];
     stats->clusterTests = seg[3];
+    stats->discardedTests = seg[4];
     stats->totalMs = ms_since(t0);
 }
 

@@ -1124,19 +1124,24 @@ __global__ __launch_bounds__(1024) void rtc_order_blocks(const unsigned *__restr
 constexpr int kSegSlots = 256, kSegSlotStride = 16; /* u64 */
 static_assert(kSegSlots * kSegSlotStride == 256 * 16, "rtc_scene_upload allocates 256 x 16 u64");
 
+/* counters (rtc.h RTC_SEGMENT_COUNTERS): [0] calculateRayCollision calls, [1] traced, [2] ray-triangle tests of
+ * the accumulated samples, [3] ray-cluster tests, [4] ray-triangle tests of speculative samples that were
+ * evaluated but not accumulated (rtc_render_chain / rtc_render_pipe / rtc_render_spec) */
 __device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned segCalls, unsigned segTraced,
-                                               unsigned long long segTests, int lane, unsigned segClusters = 0)
+                                               unsigned long long segTests, int lane, unsigned segClusters = 0,
+                                               unsigned long long segSpec = 0)
 {
     if (!P.segments)
         return;
-    unsigned long long a = segCalls, b = segTraced, n = segTests, k = segClusters;
+    unsigned long long a = segCalls, b = segTraced, n = segTests, k = segClusters, q = segSpec;
     for (int off = 32; off > 0; off >>= 1) {
         a += __shfl_xor(a, off);
         b += __shfl_xor(b, off);
         n += __shfl_xor(n, off);
         k += __shfl_xor(k, off);
+        q += __shfl_xor(q, off);
     }
-    if (lane == 0 && (a | b | n | k)) {
+    if (lane == 0 && (a | b | n | k | q)) {
         const unsigned slot = (blockIdx.x * 7u + blockIdx.y * 131u + (threadIdx.x >> 6)) % kSegSlots;
         unsigned long long *c = P.segSlots + (size_t)slot * kSegSlotStride;
         atomicAdd(&c[0], a);
@@ -1144,16 +1149,18 @@ __device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned s
         atomicAdd(&c[2], n);
         if (k)
             atomicAdd(&c[3], k);
+        if (q)
+            atomicAdd(&c[4], q);
     }
 }
 
 __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(unsigned long long *__restrict__ slots,
                                                                  unsigned long long *__restrict__ out)
 {
-    __shared__ unsigned long long part[4][kSegSlots / 64];
+    __shared__ unsigned long long part[RTC_SEGMENT_COUNTERS][kSegSlots / 64];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < RTC_SEGMENT_COUNTERS; ++k) {
         unsigned long long v = slots[(size_t)t * kSegSlotStride + k];
         slots[(size_t)t * kSegSlotStride + k] = 0; /* zero again for the next launch */
         for (int off = 32; off > 0; off >>= 1)
@@ -1162,7 +1169,7 @@ __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(unsigned long l
             part[k][w] = v;
     }
     __syncthreads();
-    if (t < 4) {
+    if (t < RTC_SEGMENT_COUNTERS) {
         unsigned long long v = 0;
         for (int i = 0; i < kSegSlots / 64; ++i)
             v += part[t][i];
@@ -1424,17 +1431,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
  * Every value is produced by the same operations as in rtc_render_kernel, only on different lanes, so the
  * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
  * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
-/* KC (the lanes per pixel, a template parameter of the heavy path) is 4 for full frames and 8 for small
- * launches (a rank's share of a multi-GPU frame, see rtc_render_rows_async): 8 lanes split the trace
- * further and evaluate the six Box-Muller transcendentals on six lanes, shortening each pixel's chain. */
-#ifndef RTC_COOP8_MAX_PIXELS
-#define RTC_COOP8_MAX_PIXELS 700000
-#endif
-/* faithful launches up to this many pixels use rtc_render_pipe (two samples in flight per pixel): a rank's
- * share of a multi-GPU 1080p or 4K frame; measured faster there, slower on a whole 1080p frame */
-#ifndef RTC_PIPE_MAX_PIXELS
-#define RTC_PIPE_MAX_PIXELS 1100000
-#endif
+/* KC (the lanes per pixel, a template parameter of the cooperative heavy kernel): 4 or 8 (RTC_F_COOP4 /
+ * RTC_F_COOP8); 8 lanes split the trace further and evaluate the six Box-Muller transcendentals on six lanes. */
 #ifndef RTC_SKY_UNROLL
 #define RTC_SKY_UNROLL 2
 #endif
@@ -2132,7 +2130,7 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int items = P.heavy[2];
-    unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segClusters = 0;
+    unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segClusters = 0, segSpec = 0;
     for (;;) {
         /* one pixel per fetch, heaviest tiles first (P.heavy[3]: the next item) */
         int it = 0;
@@ -2175,6 +2173,7 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
             V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
             int bounce = 0;
             unsigned draws = 0, calls = 0, traced = 0;
+            unsigned long long rtests = 0, rclusters = 0;
             bool live = act;
 #ifdef RTC_DIAG
             if (lane == 0)
@@ -2196,14 +2195,14 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
                             c = Closest{999999.f, -1};
                             primary_listed_lds(dir, c, mask, P.maskWords, sPF, sPX);
                             traced++;
-                            segTests += L;
+                            rtests += L;
                         }
                     } else {
                         unsigned tt = 0;
                         c = trace_clusters(P, pos, dir, sTri, sCl, tt);
                         traced++;
-                        segTests += tt;
-                        segClusters += (unsigned)P.clusterCount;
+                        rtests += tt;
+                        rclusters += (unsigned)P.clusterCount;
                     }
                     bool endSample;
                     if (c.idx >= 0) {
@@ -2240,6 +2239,10 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
             if (lane < nv) {
                 segCalls += calls;
                 segTraced += traced;
+                segTests += rtests;
+                segClusters += rclusters;
+            } else if (act) {
+                segSpec += rtests;
             }
             for (int j = 0; j < nv; ++j) { /* main.c:99, in sample order */
                 const V3 lj{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.x), j)),
@@ -2270,7 +2273,7 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
             }
         }
     }
-    flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters);
+    flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
 }
 
 __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
@@ -2278,6 +2281,207 @@ __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
     return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX));
 }
 
+
+/* ---- state-indexed samples (rtc_render_chain, the default for pixels that see geometry) --------------------
+ * A pixel's samples are chained only through its RNG state (main.c:95-100), and in the OBJ scenes every sample
+ * whose primary ray hits draws exactly 7 values per hit (RandomDiretion's six, moremath.c:104-108, and the
+ * roulette draw, raytracing.c:285) and none on a miss.  So a sample is a pure function of the draw offset it
+ * starts at: write S_j for the sample started from the seed advanced by 7 j draws (rng_advance; the LCG step
+ * is affine) and h_j for its number of hits.  The reference's k-th sample is S_{j_k} with
+ *     j_0 = 0,   j_{k+1} = j_k + h_{j_k}
+ * (h >= 1 when the primary ray hits; when it misses every sample is S_0 and h = 0).  The kernel evaluates
+ * S_j for a window of consecutive j -- one lane per j, 64 at a time -- and then walks the chain through the
+ * window, adding the members' radiance in sample order (main.c:99, sequential f32 adds).  Every accumulated
+ * value is one of the reference's samples, computed by the reference's operations from its exact start state,
+ * so the frame is bit-identical; no prediction is involved.  ~97 % of the geometry pixels of the BASELINE frame
+ * have no sample with a second hit (sum h = spp), so one window of 64 covers them; the others take a second
+ * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
+ * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
+ * Work: one wave per geometry pixel (rtc_pixel_list), statically strided over a fixed grid (no atomics). */
+constexpr int kChainBlock = 256;
+constexpr int kChainWorkers = 2048;
+#ifndef RTC_CHAIN_UNROLL
+#define RTC_CHAIN_UNROLL 2
+#endif
+#ifndef RTC_CHAIN_WAVES
+#define RTC_CHAIN_WAVES 1
+#endif
+
+/* calculateRayCollision for this lane's bounce segment over the clusters its half-line may reach (DevCluster),
+ * every record scalar-loaded: the cluster loop is wave-uniform (a cluster is visited when any lane keeps it),
+ * lanes that culled it are masked; inside, the exact-safe filter then the reference arithmetic for survivors.
+ * Ties between records of different clusters keep the lowest index (general_exact). */
+__device__ __forceinline__ Closest chain_trace_bounce(const RenderParams &P, V3 pos, V3 dir, unsigned &tests)
+{
+    Closest c{999999.f, -1};
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+    unsigned cm = 0;
+    for (int k = 0; k < P.clusterCount; ++k)
+        cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[k])) << k;
+    tests = (unsigned)__popc(cm) * kClusterSize -
+            ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+    for (int k = 0; k < P.clusterCount; ++k) {
+        if (!__ballot((cm >> k) & 1u))
+            continue;
+        if ((cm >> k) & 1u) {
+            const DevTri *R = P.clTris + k * kClusterSize;
+            unsigned surv = 0;
+#pragma unroll RTC_CHAIN_UNROLL
+            for (int j = 0; j < kClusterSize; ++j)
+                surv |= (unsigned)general_filter(pos, dir, R[j]) << j;
+            for (int j = 0; j < kClusterSize; ++j)
+                if (__ballot((surv >> j) & 1u) && ((surv >> j) & 1u))
+                    general_exact(pos, dir, R[j], __float_as_int(R[j].pad0), c);
+        }
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
+    RenderParams P)
+{
+    __shared__ PowTablesLds sPow;
+    sPow.fill(threadIdx.x);
+    __syncthreads();
+    sPow.attach(P.env);
+    const int lane = threadIdx.x & 63;
+    const int nWaves = (int)gridDim.x * (kChainBlock / 64);
+    const int gw = __builtin_amdgcn_readfirstlane((int)blockIdx.x * (kChainBlock / 64) + (int)(threadIdx.x >> 6));
+    const int items = P.heavy[2]; /* rtc_pixel_list: geometry pixels, tile * 64 + bit */
+    const int tilesX = P.blocksX * 2;
+    unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segSpec = 0, segClusters = 0;
+    for (int it = gw; it < items; it += nWaves) {
+        const int code = __builtin_amdgcn_readfirstlane(P.pixList[it]);
+        const int tile = code >> 6, bit = code & 63;
+        const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
+        const int y = P.rowStart + r * P.rowStride;
+        const V3 pdir = primary_dir(P, x, y); /* main.c:88-94 */
+        const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
+        unsigned L = 0;
+        for (int w = 0; w < P.maskWords; ++w)
+            L += (unsigned)__popcll(mask[w]);
+        const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
+        Closest prim{999999.f, -1};
+        if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
+            closest_primary_listed(P, pdir, prim, 0, mask);
+            if (lane == 0) {
+                segTraced++;
+                segTests += L;
+            }
+        }
+        V3 acc{0.f, 0.f, 0.f};
+        int k = 0;       /* samples accumulated */
+        unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
+        while (k < P.spp && P.maxBounce > 0) {
+            const int need = P.spp - k;
+            const int nAct = min(64, need + (need >> 4) + 1);
+            const bool act = lane < nAct;
+            unsigned rng = rng_advance(seed, 7u * (jn + (unsigned)lane));
+            /* ---- S_{jn + lane}: one calcColor (raytracing.c:262-296) ---- */
+            V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+            int bounce = 0;
+            unsigned hits = 0, calls = 0, tests = 0, clTests = 0;
+            bool alive = act;
+            while (__any(alive)) {
+                if (alive) {
+                    Closest c;
+                    calls++;
+                    if (bounce == 0) { /* every live lane: the pixel's primary ray */
+                        if (P.hoist) {
+                            c = prim;
+                        } else {
+                            c = Closest{999999.f, -1};
+                            closest_primary_listed(P, dir, c, 0, mask);
+                            tests += L;
+                        }
+                    } else {
+                        unsigned t = 0;
+                        c = chain_trace_bounce(P, pos, dir, t);
+                        tests += t;
+                        clTests += (unsigned)P.clusterCount;
+                    }
+                    bool endSample;
+                    if (c.idx >= 0) {
+                        hits++;
+                        /* calcColor hit branch, raytracing.c:272-287 */
+                        const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
+                        const DevTri &T = P.tris[c.idx];
+                        const DevMat M = P.mats[c.idx];
+                        const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+                        const V3 specularDir = reflect(dir, normal);
+                        dir = lerp(diffuseDir, specularDir, M.smoothness);
+                        pos = hitPoint;
+                        const V3 emitted = mul(color, M.emission);
+                        light = add(light, mulv(emitted, rayColor));
+                        rayColor = mulv(rayColor, color);
+                        const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                        endSample = p < random_value(rng);
+                        if (!endSample) {
+                            rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
+                            bounce++;
+                            endSample = bounce >= P.maxBounce;
+                        }
+                    } else {
+                        light = add(light, mulv(environment(dir, P.env), rayColor)); /* raytracing.c:291 */
+                        endSample = true;
+                    }
+                    if (endSample)
+                        alive = false;
+                }
+            }
+            /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
+            const V3 t = mul(light, P.invSpp);
+            const unsigned long long ones = __ballot(act && hits == 1u);
+            unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
+            int p = 0;
+            while (k < P.spp && p < nAct) {
+                const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
+                const unsigned long long notOne = ~ones & win;
+                const int q = notOne ? __builtin_ctzll(notOne) : nAct;
+                const int take = min(q - p, P.spp - k);
+                for (int b = p; b < p + take; ++b) { /* a run of one-hit samples: j advances by 1 */
+                    acc.x = acc.x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), b));
+                    acc.y = acc.y + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), b));
+                    acc.z = acc.z + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), b));
+                }
+                mult += (lane >= p && lane < p + take) ? 1u : 0u;
+                k += take;
+                p += take;
+                if (k >= P.spp || p != q || q >= nAct)
+                    break;
+                /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
+                acc.x = acc.x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q));
+                acc.y = acc.y + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q));
+                acc.z = acc.z + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q));
+                mult += lane == q ? 1u : 0u;
+                k++;
+                p = q + __builtin_amdgcn_readlane((int)hits, q);
+            }
+            jn += (unsigned)p;
+            /* counters: committed samples (with multiplicity) and the tests of the discarded ones */
+            segCalls += (unsigned long long)mult * calls;
+            segTraced += (unsigned long long)mult * (P.hoist ? calls - 1u : calls);
+            segTests += (unsigned long long)mult * tests;
+            segClusters += (unsigned long long)mult * clTests;
+            if (act && mult == 0)
+                segSpec += tests;
+        }
+        if (lane == 0) {
+            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
+            P.colors[3 * o] = float_to_u8(acc.x);
+            P.colors[3 * o + 1] = float_to_u8(acc.y);
+            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (P.accum) {
+                P.accum[3 * o] = acc.x;
+                P.accum[3 * o + 1] = acc.y;
+                P.accum[3 * o + 2] = acc.z;
+            }
+        }
+    }
+    flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
+}
 
 /* ---- two samples in flight per pixel (rtc_render_pipe) ----------------------------------------------------
  * A pixel's samples are chained only through the RNG state (main.c:95-100).  Here each pixel has two 4-lane
@@ -2323,7 +2527,7 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
     const int groupBase = lane & ~(KC - 1);
     const int g = (lane >> 2) & 1; /* which of the pixel's two groups */
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
-    unsigned long long segTests = 0;
+    unsigned long long segTests = 0, segEval = 0;
     const int heavy = P.heavy[0];
     for (;;) {
         if (threadIdx.x == 0)
@@ -2365,7 +2569,7 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
 
         /* this group's sample */
         int n = -1;
-        unsigned st0 = 0, rng = 0, draws = 0, calls = 0, traced = 0;
+        unsigned st0 = 0, rng = 0, draws = 0, calls = 0, traced = 0, tests = 0, clTests = 0;
         int fin = 1, isCur = g == 0, bounce = 0;
         V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
         auto start = [&](int ns, unsigned s0) {
@@ -2377,7 +2581,7 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
                 n = -1;
                 fin = 1;
             }
-            draws = calls = traced = 0;
+            draws = calls = traced = tests = clTests = 0;
             bounce = 0;
             pos = P.origin;
             dir = pdir;
@@ -2386,7 +2590,7 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
         };
         /* the pixel (replicated on its 8 lanes) */
         V3 acc{0.f, 0.f, 0.f};
-        unsigned pixCalls = 0, pixTraced = 0;
+        unsigned pixCalls = 0, pixTraced = 0, pixTests = 0, pixClusters = 0;
         int committed = 0;
         bool pixDone = !(valid && P.spp > 0 && P.maxBounce > 0);
         if (!pixDone) {
@@ -2405,10 +2609,10 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
                 const bool listed = bounce == 0;
                 c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
                 traced++;
-                if (sub == 0) {
-                    segTests += listed ? L : nc;
-                    segClusters += listed ? 0u : (unsigned)P.clusterCount;
-                }
+                tests += listed ? L : nc;
+                clTests += listed ? 0u : (unsigned)P.clusterCount;
+                if (sub == 0) /* every test evaluated (accumulated or not); the accumulated ones go to [2] below */
+                    segEval += listed ? L : nc;
                 bool endSample;
                 if (c.idx >= 0) {
                     const V3 hitPoint = add(pos, mul(dir, c.dst));
@@ -2440,7 +2644,8 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
             const int oN = pipe_other_i(n), oFin = pipe_other_i(fin), oCur = pipe_other_i(isCur);
             const unsigned oSt0 = (unsigned)pipe_other_i((int)st0), oRng = (unsigned)pipe_other_i((int)rng);
             const unsigned oDraws = (unsigned)pipe_other_i((int)draws), oCalls = (unsigned)pipe_other_i((int)calls),
-                           oTraced = (unsigned)pipe_other_i((int)traced);
+                           oTraced = (unsigned)pipe_other_i((int)traced), oTests = (unsigned)pipe_other_i((int)tests),
+                           oClTests = (unsigned)pipe_other_i((int)clTests);
             const V3 oLight{pipe_other_f(light.x), pipe_other_f(light.y), pipe_other_f(light.z)};
             (void)oCur;
             const bool me = isCur != 0;
@@ -2454,6 +2659,8 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
                 acc = add(acc, mul(cLight, P.invSpp)); /* main.c:99: sample cN */
                 pixCalls += me ? calls : oCalls;
                 pixTraced += me ? traced : oTraced;
+                pixTests += me ? tests : oTests;
+                pixClusters += me ? clTests : oClTests;
                 committed++;
                 unsigned e = cRng, D = cDraws == 0u ? 0u : 7u;
                 const bool sValid = sN == cN + 1 && sSt0 == e;
@@ -2461,6 +2668,8 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
                     acc = add(acc, mul(sLight, P.invSpp)); /* sample cN + 1 */
                     pixCalls += me ? oCalls : calls;
                     pixTraced += me ? oTraced : traced;
+                    pixTests += me ? oTests : tests;
+                    pixClusters += me ? oClTests : clTests;
                     committed++;
                     e = sRng;
                     D = sDraws == 0u ? 0u : 7u;
@@ -2505,10 +2714,13 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
             }
             segCalls += pixCalls;
             segTraced += pixTraced;
+            segTests += pixTests;
+            segClusters += pixClusters;
         }
         __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
     }
-    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
+    /* discarded = evaluated - accumulated, summed over the wave (u64 wrap-around per lane is exact in the sum) */
+    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segEval - segTests);
 }
 
 static EnvParams env_of(const Scene &s)
@@ -2536,6 +2748,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                         d->rowStart, d->rowStride);
     if ((long long)d->width * d->height > (1ll << 31) / 4)
         return rtc_fail(RTC_EINVAL, "frame too large");
+    {
+        const int f = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
+        if (f & (f - 1))
+            return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_COOP4 / COOP8 / PIPE / SPEC are exclusive");
+        if ((d->flags & RTC_F_PIPE) && (d->flags & RTC_F_HOIST_PRIMARY))
+            return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_PIPE runs faithful launches only");
+    }
     const int rows = rtc_rows_selected(d);
     if (rows == 0)
         return 0;
@@ -2629,8 +2848,12 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
             P.order = order;
             P.heavy = heavy;
-            const bool spec = (d->flags & RTC_F_SPEC) != 0;
-            if (spec) {
+            /* the heavy-tile kernel: rtc_render_chain by default; the older cooperative kernels on request
+             * (A/B timing; every variant gives the same frame) */
+            const int forced = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
+            const bool spec = forced == RTC_F_SPEC;
+            const bool chain = forced == 0;
+            if (spec || chain) {
                 int *pixList = heavy + 4;
                 hipLaunchKernelGGL(rtc_pixel_list, dim3(1), dim3(1024), 0, st, (const int *)order, (const unsigned long long *)pixMask,
                                    heavy, pixList);
@@ -2656,12 +2879,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
             const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
-            /* small launches: 8 lanes per pixel (shorter chains; see KC) */
-            const bool eight = (d->flags & RTC_F_COOP8) ||
-                               (!(d->flags & RTC_F_COOP4) && (size_t)d->width * (size_t)rows <= (size_t)RTC_COOP8_MAX_PIXELS);
-            const bool pipe = !(d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_NO_PIPE)) && !P.hoist &&
-                              ((d->flags & RTC_F_PIPE) || (size_t)d->width * (size_t)rows <= (size_t)RTC_PIPE_MAX_PIXELS);
-            if (spec)
+            const bool eight = forced == RTC_F_COOP8;
+            const bool pipe = forced == RTC_F_PIPE;
+            if (chain)
+                hipLaunchKernelGGL(rtc_render_chain, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
+            else if (spec)
                 hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
             else if (pipe)
                 hipLaunchKernelGGL(rtc_render_pipe, workers, dim3(512), rtc_heavy_lds_bytes(s->triPadded), st, P);

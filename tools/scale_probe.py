@@ -26,7 +26,7 @@ seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
 base = None
 for n in (1, 2, 4, 8):
     for r, lanes in [(0, 0), (0, -1)]:
-        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, pipe=1 if lanes == 0 else -1)
+        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, pipe=(lanes == 0))
         times, kts = [], []
         for _ in range(frames):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
