@@ -468,6 +468,12 @@ struct RenderParams {
     int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter),
                                       [2] geometry pixels in pixList */
     const int *__restrict__ pixList; /* geometry pixels of the heavy tiles, heaviest tile first: tile*64 + bit */
+    /* rtc_render_chain's work: kGeoLists sub-lists of geometry pixels (tile*64 + bit), filled by rtc_tile_cull
+     * (tile t appends to sub-list t % kGeoLists, one atomic per tile with geometry, spread over kGeoLists
+     * counters in separate cache lines); geoCount[l * 32] = entries of sub-list l, zeroed by rtc_prep_primary */
+    int *__restrict__ geoCount;
+    int *__restrict__ geoList;
+    int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
@@ -484,6 +490,7 @@ struct RenderParams {
 };
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
+constexpr int kGeoLists = 16, kGeoCountStride = 32; /* ints: one 128-B line per counter */
 
 /* The pixel a lane renders and its primary ray (rowThread, main.c:88-94).  A 256-thread workgroup covers
  * 16x16 pixels of the launch's rows; wave w of it the 8x8 tile (w & 1, w >> 1). */
@@ -545,9 +552,12 @@ __device__ __forceinline__ void block_xy(const RenderParams &P, int &bx, int &by
  * three bounds above, the subtraction error and 2^-21 |AB|_1 |AC|_1 (>= |det|).  Every bound is taken 4x and rounded up; the sign tests also carry 2^-60
  * so a product that could round to -0 is never treated as negative. */
 __global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict__ tris, DevPrimF *__restrict__ pf,
-                                                        DevPrimX *__restrict__ px, int triCount, V3 origin)
+                                                        DevPrimX *__restrict__ px, int triCount, V3 origin,
+                                                        int *__restrict__ geoCount)
 {
     const int t = blockIdx.x * 64 + threadIdx.x;
+    if (geoCount && blockIdx.x == 0 && threadIdx.x < kGeoLists) /* the launch's geometry sub-lists start empty */
+        geoCount[threadIdx.x * kGeoCountStride] = 0;
     if (t >= triCount)
         return;
     const DevTri T = tris[t];
@@ -1083,6 +1093,16 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     if (lane == 0) {
         tileW[tile] = (unsigned)__popcll(b);
         pixMask[tile] = b;
+    }
+    if (P.geoList && b) {
+        /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work) */
+        const int l = tile % kGeoLists;
+        int base = 0;
+        if (lane == 0)
+            base = atomicAdd(&P.geoCount[l * kGeoCountStride], __popcll(b));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if ((b >> lane) & 1ull)
+            P.geoList[(size_t)l * P.geoCap + base + __popcll(b & ((1ull << lane) - 1ull))] = tile * 64 + lane;
     }
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
@@ -2304,36 +2324,90 @@ constexpr int kChainWorkers = 2048;
 #define RTC_CHAIN_UNROLL 2
 #endif
 #ifndef RTC_CHAIN_WAVES
-#define RTC_CHAIN_WAVES 1
+#define RTC_CHAIN_WAVES 4
 #endif
 
-/* calculateRayCollision for this lane's bounce segment over the clusters its half-line may reach (DevCluster),
- * every record scalar-loaded: the cluster loop is wave-uniform (a cluster is visited when any lane keeps it),
- * lanes that culled it are masked; inside, the exact-safe filter then the reference arithmetic for survivors.
- * Ties between records of different clusters keep the lowest index (general_exact). */
-__device__ __forceinline__ Closest chain_trace_bounce(const RenderParams &P, V3 pos, V3 dir, unsigned &tests)
+/* The bounce segments of a wave's lanes (calculateRayCollision, raytracing.c:216-240), as a dense list of
+ * (lane, cluster) pairs.  Each live lane culls the clusters its half-line cannot reach (DevCluster bound) and
+ * enters the rest into the wave's pair list (cluster-major); the list is then processed 64 pairs at a time,
+ * every lane taking one pair: the owner's ray from LDS, the cluster's 8 records from LDS (staged once per
+ * workgroup), the exact-safe filter and the reference arithmetic for survivors.  A pair's closest hit goes
+ * to its owner with an LDS atomic minimum on (dst bits << 32 | index): dst >= EPSILON > 0, so the float bits
+ * order like the values and the key order is the lexicographic (dst, index) order -- the lowest index among
+ * equal distances, as the reference's strict `<` over ascending indices keeps (raytracing.c:231).  Only
+ * candidates with dst < 999999 (the reference's initial closest distance, raytracing.c:218) enter.
+ * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
+ * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
+struct ChainWaveLds {
+    float4 ray[64][2];            /* pos, dir of each lane's segment */
+    unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
+    unsigned short pair[64 * 32]; /* lane | cluster << 6, cluster-major */
+};
+constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
+static_assert(kCoopMaxTris / kClusterSize <= 32, "the pair list holds 32 clusters per lane");
+
+__device__ __forceinline__ void wave_lds_sync()
 {
-    Closest c{999999.f, -1};
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
-    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, V3 pos, V3 dir,
+                                                     const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
+                                                     unsigned &tests)
+{
+    W.ray[lane][0] = make_float4(pos.x, pos.y, pos.z, 0.f);
+    W.ray[lane][1] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    W.key[lane] = kNoHitKey;
     unsigned cm = 0;
-    for (int k = 0; k < P.clusterCount; ++k)
-        cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[k])) << k;
-    tests = (unsigned)__popc(cm) * kClusterSize -
-            ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+    if (alive) {
+        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+        const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+        for (int k = 0; k < P.clusterCount; ++k)
+            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[k])) << k;
+        tests = (unsigned)__popc(cm) * kClusterSize -
+                ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+    }
+    int n = 0;
     for (int k = 0; k < P.clusterCount; ++k) {
-        if (!__ballot((cm >> k) & 1u))
-            continue;
-        if ((cm >> k) & 1u) {
-            const DevTri *R = P.clTris + k * kClusterSize;
+        const unsigned long long m = __ballot((cm >> k) & 1u);
+        if ((cm >> k) & 1u)
+            W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                (unsigned short)(lane | (k << 6));
+        n += (int)__popcll(m);
+    }
+    wave_lds_sync();
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        if (i < n) {
+            const unsigned pr = W.pair[i];
+            const int o = (int)(pr & 63u), k = (int)(pr >> 6);
+            const float4 rp = W.ray[o][0], rd = W.ray[o][1];
+            const V3 rpos{rp.x, rp.y, rp.z}, rdir{rd.x, rd.y, rd.z};
+            const DevTri *R = sRec + k * kClusterSize;
             unsigned surv = 0;
 #pragma unroll RTC_CHAIN_UNROLL
             for (int j = 0; j < kClusterSize; ++j)
-                surv |= (unsigned)general_filter(pos, dir, R[j]) << j;
-            for (int j = 0; j < kClusterSize; ++j)
-                if (__ballot((surv >> j) & 1u) && ((surv >> j) & 1u))
-                    general_exact(pos, dir, R[j], __float_as_int(R[j].pad0), c);
+                surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
+            if (surv) {
+                Closest c{999999.f, -1};
+                while (surv) {
+                    const int j = __builtin_ctz(surv);
+                    surv &= surv - 1;
+                    general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
+                }
+                if (c.idx >= 0 && c.dst < 999999.f)
+                    atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
+            }
         }
+    }
+    wave_lds_sync();
+    const unsigned long long key = W.key[lane];
+    Closest c{999999.f, -1};
+    if (key != kNoHitKey) {
+        c.dst = __uint_as_float((unsigned)(key >> 32));
+        c.idx = (int)(unsigned)key;
     }
     return c;
 }
@@ -2341,18 +2415,33 @@ __device__ __forceinline__ Closest chain_trace_bounce(const RenderParams &P, V3 
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
+    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
+    __shared__ ChainWaveLds sWave[kChainBlock / 64];
+    DevTri *sRec = (DevTri *)sDyn; /* the clustered scene records (clusterCount * 8; pad0 = reference index) */
     sPow.fill(threadIdx.x);
+    for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
+        sRec[i] = P.clTris[i];
     __syncthreads();
     sPow.attach(P.env);
     const int lane = threadIdx.x & 63;
+    ChainWaveLds &W = sWave[threadIdx.x >> 6];
     const int nWaves = (int)gridDim.x * (kChainBlock / 64);
     const int gw = __builtin_amdgcn_readfirstlane((int)blockIdx.x * (kChainBlock / 64) + (int)(threadIdx.x >> 6));
-    const int items = P.heavy[2]; /* rtc_pixel_list: geometry pixels, tile * 64 + bit */
+    /* the geometry pixels: kGeoLists sub-lists from rtc_tile_cull, taken as one concatenated index space
+     * (l: the sub-list of item `it`, base: its first item, cnt: its length) */
     const int tilesX = P.blocksX * 2;
     unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segSpec = 0, segClusters = 0;
-    for (int it = gw; it < items; it += nWaves) {
-        const int code = __builtin_amdgcn_readfirstlane(P.pixList[it]);
+    int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
+    for (int it = gw;; it += nWaves) {
+        while (it - base >= cnt && l < kGeoLists - 1) {
+            base += cnt;
+            ++l;
+            cnt = __builtin_amdgcn_readfirstlane(P.geoCount[l * kGeoCountStride]);
+        }
+        if (it - base >= cnt)
+            break;
+        const int code = __builtin_amdgcn_readfirstlane(P.geoList[(size_t)l * P.geoCap + (it - base)]);
         const int tile = code >> 6, bit = code & 63;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
         const int y = P.rowStart + r * P.rowStride;
@@ -2383,24 +2472,27 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             int bounce = 0;
             unsigned hits = 0, calls = 0, tests = 0, clTests = 0;
             bool alive = act;
-            while (__any(alive)) {
-                if (alive) {
-                    Closest c;
-                    calls++;
-                    if (bounce == 0) { /* every live lane: the pixel's primary ray */
+            for (bool first = true; __any(alive); first = false) {
+                Closest c{999999.f, -1};
+                if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
+                    if (alive) {
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            c = Closest{999999.f, -1};
                             closest_primary_listed(P, dir, c, 0, mask);
                             tests += L;
                         }
-                    } else {
-                        unsigned t = 0;
-                        c = chain_trace_bounce(P, pos, dir, t);
+                    }
+                } else { /* bounce segments of the live lanes (the whole wave takes part) */
+                    unsigned t = 0;
+                    c = chain_trace_pairs(P, alive, pos, dir, sRec, W, lane, t);
+                    if (alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
                     }
+                }
+                if (alive) {
+                    calls++;
                     bool endSample;
                     if (c.idx >= 0) {
                         hits++;
@@ -2431,6 +2523,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         alive = false;
                 }
             }
+            (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
             const V3 t = mul(light, P.invSpp);
             const unsigned long long ones = __ballot(act && hits == 1u);
@@ -2808,9 +2901,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                        !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
+    const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64);
     if (cull) {
         const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int) +
-                            tiles * 64 * sizeof(int); /* + the geometry pixel list */
+                            tiles * 64 * sizeof(int) /* + the geometry pixel list */ +
+                            (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int); /* + sub-lists */
         if (need > s->scratchCap) {
             RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (ms->scratch)
@@ -2830,30 +2925,37 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         }
         return 0;
     };
-    if (s->triPadded > 0)
+    /* the heavy-tile kernel of the split launch: rtc_render_chain unless one of the older ones is forced */
+    const int forced = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
+    const bool chain = fused && forced == 0;
+    unsigned long long *mask = cull ? (unsigned long long *)s->scratch : nullptr;
+    unsigned long long *pixMask = cull ? mask + tiles * (size_t)s->maskWords : nullptr;
+    unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
+    unsigned *tileW = cull ? weight + blocks : nullptr;
+    int *order = cull ? (int *)(tileW + tiles) : nullptr;
+    if (chain) {
+        P.geoCount = order + tiles + blocks + 4 + tiles * 64;
+        P.geoList = P.geoCount + kGeoLists * kGeoCountStride;
+        P.geoCap = geoCap;
+    }
+    if (s->triPadded > 0 || chain)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
-                           s->primF, s->primX, s->triPadded + 8, P.origin);
+                           s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, P.geoCount);
     if (cull) {
-        unsigned long long *mask = (unsigned long long *)s->scratch;
-        unsigned long long *pixMask = mask + tiles * (size_t)s->maskWords;
-        unsigned *weight = (unsigned *)(pixMask + tiles);
-        unsigned *tileW = weight + blocks;
-        int *order = (int *)(tileW + tiles);
         hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW, pixMask);
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {
-            /* sky tiles on the side stream, concurrently with the heavy tiles on `st`; `st` then waits for both */
+            /* sky tiles on the side stream, concurrently with the heavy tiles on `st`; `st` then waits for both.
+             * The older heavy kernels take the heavy tiles heaviest first (rtc_order_heavy); rtc_render_chain
+             * takes the geometry pixels from the tile cull's sub-lists */
             int *heavy = order + tiles + blocks;
-            hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
+            if (!chain)
+                hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
             P.order = order;
             P.heavy = heavy;
-            /* the heavy-tile kernel: rtc_render_chain by default; the older cooperative kernels on request
-             * (A/B timing; every variant gives the same frame) */
-            const int forced = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
             const bool spec = forced == RTC_F_SPEC;
-            const bool chain = forced == 0;
-            if (spec || chain) {
+            if (spec) {
                 int *pixList = heavy + 4;
                 hipLaunchKernelGGL(rtc_pixel_list, dim3(1), dim3(1024), 0, st, (const int *)order, (const unsigned long long *)pixMask,
                                    heavy, pixList);
@@ -2882,7 +2984,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const bool eight = forced == RTC_F_COOP8;
             const bool pipe = forced == RTC_F_PIPE;
             if (chain)
-                hipLaunchKernelGGL(rtc_render_chain, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
+                hipLaunchKernelGGL(rtc_render_chain, dim3(kChainWorkers), dim3(kChainBlock),
+                                   (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
             else if (spec)
                 hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
             else if (pipe)

@@ -43,8 +43,8 @@ if os.path.exists(path):
 entry = {"n_gpus": 1, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/one_render.py faithful",
          "kernels": {}}
 for k in sorted(set(fetch) | set(write)):
-    if not any(s in k for s in ("rtc_render_heavy", "rtc_render_sky", "rtc_tile_cull", "rtc_prep_primary",
-                                "rtc_order_heavy", "rtc_reduce_segments")):
+    if not any(s in k for s in ("rtc_render_heavy", "rtc_render_chain", "rtc_render_sky", "rtc_tile_cull",
+                                "rtc_prep_primary", "rtc_order_heavy", "rtc_pixel_list", "rtc_reduce_segments")):
         continue
     f = fetch.get(k, [])
     w = write.get(k, [])
@@ -52,10 +52,12 @@ for k in sorted(set(fetch) | set(write)):
     wk = sum(w) / len(w) if w else 0.0
     entry["kernels"][k] = {"fetch_kb_raw": round(fk, 3), "write_kb": round(wk, 3), "dispatches": max(len(f), len(w)),
                            "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024)}
-heavy = [v for k, v in entry["kernels"].items() if "rtc_render_heavy" in k]
-if heavy:
-    entry["kernel"] = "rtc_render_heavy"
-    entry["hbm_bytes_per_launch"] = heavy[0]["hbm_bytes_per_launch"]
+for name in ("rtc_render_chain", "rtc_render_heavy"):  # the split launch's heavy-tile kernel
+    heavy = [v for k, v in entry["kernels"].items() if name in k]
+    if heavy:
+        entry["kernel"] = name
+        entry["hbm_bytes_per_launch"] = heavy[0]["hbm_bytes_per_launch"]
+        break
 out[workload] = entry
 os.makedirs(os.path.dirname(path), exist_ok=True)
 json.dump(out, open(path, "w"), indent=1)
