@@ -116,6 +116,16 @@ __device__ __forceinline__ unsigned rng_advance(unsigned s, unsigned k)
             s = s * T.j[b].a + T.j[b].c;
     return s;
 }
+/* the affine map of k draws as (a, c): rng_advance(s, k) == s * a + c */
+__device__ __forceinline__ RngJump rng_jump_by(unsigned k)
+{
+    constexpr RngPow2Table T;
+    RngJump j{1u, 0u};
+    for (int b = 0; b < 32 && (k >> b) != 0u; ++b)
+        if ((k >> b) & 1u)
+            j = rng_compose(j, T.j[b]);
+    return j;
+}
 __device__ __forceinline__ float rng_value_of_state(unsigned s)
 {
     unsigned r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;

@@ -2338,6 +2338,7 @@ constexpr int kChainWorkers = 2048;
  * candidates with dst < 999999 (the reference's initial closest distance, raytracing.c:218) enter.
  * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
+typedef float f2 __attribute__((ext_vector_type(2)));
 struct ChainWaveLds {
     float4 ray[64][2];            /* pos, dir of each lane's segment */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
@@ -2361,6 +2362,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     W.ray[lane][1] = make_float4(dir.x, dir.y, dir.z, 0.f);
     W.key[lane] = kNoHitKey;
     unsigned cm = 0;
+    DSECT_BEGIN(dc3);
     if (alive) {
         const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
         const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
@@ -2369,6 +2371,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         tests = (unsigned)__popc(cm) * kClusterSize -
                 ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
     }
+    DSECT_END(dc3, 3);
+    DSECT_BEGIN(dc4);
     int n = 0;
     for (int k = 0; k < P.clusterCount; ++k) {
         const unsigned long long m = __ballot((cm >> k) & 1u);
@@ -2378,6 +2382,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         n += (int)__popcll(m);
     }
     wave_lds_sync();
+    DSECT_END(dc4, 4);
+    DSECT_BEGIN(dc5);
     for (int b = 0; b < n; b += 64) {
         const int i = b + lane;
         if (i < n) {
@@ -2409,6 +2415,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         c.dst = __uint_as_float((unsigned)(key >> 32));
         c.idx = (int)(unsigned)key;
     }
+    DSECT_END(dc5, 5);
     return c;
 }
 
@@ -2422,10 +2429,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     sPow.fill(threadIdx.x);
     for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
         sRec[i] = P.clTris[i];
+#ifdef RTC_DIAG
+    if ((threadIdx.x & 63) < 8)
+        s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+#endif
     __syncthreads();
     sPow.attach(P.env);
     const int lane = threadIdx.x & 63;
     ChainWaveLds &W = sWave[threadIdx.x >> 6];
+    const RngJump laneJump = rng_jump_by(7u * (unsigned)lane); /* s -> the state 7 lane draws later */
     const int nWaves = (int)gridDim.x * (kChainBlock / 64);
     const int gw = __builtin_amdgcn_readfirstlane((int)blockIdx.x * (kChainBlock / 64) + (int)(threadIdx.x >> 6));
     /* the geometry pixels: kGeoLists sub-lists from rtc_tile_cull, taken as one concatenated index space
@@ -2459,14 +2471,20 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 segTests += L;
             }
         }
-        V3 acc{0.f, 0.f, 0.f};
+        f2 accxy{0.f, 0.f}; /* the pixel's accumulator (main.c:97): x, y packed, z */
+        float accz = 0.f;
         int k = 0;       /* samples accumulated */
         unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
         while (k < P.spp && P.maxBounce > 0) {
             const int need = P.spp - k;
             const int nAct = min(64, need + (need >> 4) + 1);
             const bool act = lane < nAct;
-            unsigned rng = rng_advance(seed, 7u * (jn + (unsigned)lane));
+            DSECT_BEGIN(dc0);
+            /* the lane's start state: the seed advanced by 7 (jn + lane) draws = the wave-uniform state at jn,
+             * then this lane's fixed jump by 7 lane draws (both affine LCG compositions, rng_advance) */
+            const unsigned s0 = (unsigned)__builtin_amdgcn_readfirstlane((int)rng_advance(seed, 7u * jn));
+            unsigned rng = s0 * laneJump.a + laneJump.c;
+            DSECT_END(dc0, 0);
             /* ---- S_{jn + lane}: one calcColor (raytracing.c:262-296) ---- */
             V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
             int bounce = 0;
@@ -2475,6 +2493,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             for (bool first = true; __any(alive); first = false) {
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
+                    DSECT_BEGIN(dc1);
                     if (alive) {
                         if (P.hoist) {
                             c = prim;
@@ -2483,6 +2502,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             tests += L;
                         }
                     }
+                    DSECT_END(dc1, 1);
                 } else { /* bounce segments of the live lanes (the whole wave takes part) */
                     unsigned t = 0;
                     c = chain_trace_pairs(P, alive, pos, dir, sRec, W, lane, t);
@@ -2495,6 +2515,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     calls++;
                     bool endSample;
                     if (c.idx >= 0) {
+                        DSECT_BEGIN(dc2);
                         hits++;
                         /* calcColor hit branch, raytracing.c:272-287 */
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
@@ -2515,9 +2536,12 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             bounce++;
                             endSample = bounce >= P.maxBounce;
                         }
+                        DSECT_END(dc2, 2);
                     } else {
+                        DSECT_BEGIN(dc6);
                         light = add(light, mulv(environment(dir, P.env), rayColor)); /* raytracing.c:291 */
                         endSample = true;
+                        DSECT_END(dc6, 6);
                     }
                     if (endSample)
                         alive = false;
@@ -2525,7 +2549,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             }
             (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
+            DSECT_BEGIN(dc7);
             const V3 t = mul(light, P.invSpp);
+            /* every lane's calcColor(...) * (float)(1./spp) into LDS (the ray slots are free now); the walk reads the
+             * members back with uniform (broadcast) LDS reads and adds them in sample order, x and y as one packed
+             * f32 add (two IEEE adds) */
+            W.ray[lane][0] = make_float4(t.x, t.y, t.z, 0.f);
+            wave_lds_sync();
             const unsigned long long ones = __ballot(act && hits == 1u);
             unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
             int p = 0;
@@ -2534,10 +2564,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 const unsigned long long notOne = ~ones & win;
                 const int q = notOne ? __builtin_ctzll(notOne) : nAct;
                 const int take = min(q - p, P.spp - k);
+#pragma unroll 8
                 for (int b = p; b < p + take; ++b) { /* a run of one-hit samples: j advances by 1 */
-                    acc.x = acc.x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), b));
-                    acc.y = acc.y + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), b));
-                    acc.z = acc.z + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), b));
+                    const float4 v = W.ray[b][0];
+                    accxy = accxy + f2{v.x, v.y};
+                    accz = accz + v.z;
                 }
                 mult += (lane >= p && lane < p + take) ? 1u : 0u;
                 k += take;
@@ -2545,13 +2576,14 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 if (k >= P.spp || p != q || q >= nAct)
                     break;
                 /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
-                acc.x = acc.x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q));
-                acc.y = acc.y + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q));
-                acc.z = acc.z + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q));
+                const float4 v = W.ray[q][0];
+                accxy = accxy + f2{v.x, v.y};
+                accz = accz + v.z;
                 mult += lane == q ? 1u : 0u;
                 k++;
                 p = q + __builtin_amdgcn_readlane((int)hits, q);
             }
+            wave_lds_sync(); /* the ray slots are rewritten by the next round */
             jn += (unsigned)p;
             /* counters: committed samples (with multiplicity) and the tests of the discarded ones */
             segCalls += (unsigned long long)mult * calls;
@@ -2560,19 +2592,24 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             segClusters += (unsigned long long)mult * clTests;
             if (act && mult == 0)
                 segSpec += tests;
+            DSECT_END(dc7, 7);
         }
         if (lane == 0) {
             const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(acc.x);
-            P.colors[3 * o + 1] = float_to_u8(acc.y);
-            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            P.colors[3 * o] = float_to_u8(accxy.x);
+            P.colors[3 * o + 1] = float_to_u8(accxy.y);
+            P.colors[3 * o + 2] = float_to_u8(accz);
             if (P.accum) {
-                P.accum[3 * o] = acc.x;
-                P.accum[3 * o + 1] = acc.y;
-                P.accum[3 * o + 2] = acc.z;
+                P.accum[3 * o] = accxy.x;
+                P.accum[3 * o + 1] = accxy.y;
+                P.accum[3 * o + 2] = accz;
             }
         }
     }
+#ifdef RTC_DIAG
+    if (lane < 8)
+        atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
+#endif
     flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
 }
 

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Section cycles of rtc_render_chain from the diagnostic build (librtc_diag.so, s_memtime stamps summed over
+waves), on the BASELINE frame.  Not part of the product."""
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+os.environ["RTC_LIB_PATH"] = os.path.join(REPO, "raytracingc_amd", "_lib", "librtc_diag.so")
+import raytracingc_amd as rt  # noqa: E402
+from conftest import load_tris  # noqa: E402
+
+tris, _ = load_tris("ultracomplex")
+L = rt.lib()
+L.rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
+out = (C.c_ulonglong * 16)()
+names = ["rng_setup", "primary_trace", "hit_shading", "cluster_cull", "pair_build", "pair_passes", "env", "walk"]
+for hoist in (False, True):
+    cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist)
+    rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+    L.rtc_diag_sections(out, 1)
+    _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+    L.rtc_diag_sections(out, 1)
+    tot = sum(out[i] for i in range(8))
+    print(json.dumps({"hoist": hoist, "render_ms": round(st["render_ms"], 3),
+                      "share": {n: round(out[i] / tot, 4) for i, n in enumerate(names)},
+                      "cycles": {n: int(out[i]) for i, n in enumerate(names)}}), flush=True)

@@ -10,7 +10,7 @@ import os
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcb"
-kernels = sys.argv[2:] or ["rtc_render_heavy", "rtc_render_sky"]
+kernels = sys.argv[2:] or ["rtc_render_chain", "rtc_render_heavy", "rtc_render_sky", "rtc_tile_cull"]
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
