@@ -75,6 +75,8 @@ typedef struct RtcRenderDesc {
 #define RTC_F_PIPE          0x200 /* two samples in flight per pixel (faithful launches only: with
                                      RTC_F_HOIST_PRIMARY it is RTC_EINVAL) */
 #define RTC_F_SPEC          0x100 /* sample-parallel speculation verified in sample order (lanes = samples) */
+#define RTC_F_CHAIN_INLINE  0x400 /* rtc_render_chain adds each pixel's samples itself instead of deferring the
+                                     in-order sum to a separate pass (A/B timing; identical frame) */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render launch (slowest device), HIP events */

@@ -31,6 +31,7 @@ from ._abi import (  # noqa: F401
     RTC_F_NO_CLUSTER_CULL,
     RTC_F_NO_COOP,
     RTC_F_PIPE,
+    RTC_F_CHAIN_INLINE,
     RTC_F_SPEC,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
@@ -142,13 +143,15 @@ class RenderConfig:
     coop_lanes: int = 0  # 4 or 8: the cooperative kernel with that many lanes per pixel
     spec: bool = False  # the sample-parallel speculative kernel
     pipe: bool = False  # two samples in flight per pixel (faithful only)
+    chain_inline: bool = False  # rtc_render_chain sums each pixel's samples itself (no deferred pass)
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
                 | (RTC_F_COOP4 if self.coop_lanes == 4 else 0) | (RTC_F_COOP8 if self.coop_lanes == 8 else 0)
-                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe else 0))
+                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe else 0)
+                | (RTC_F_CHAIN_INLINE if self.chain_inline else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),

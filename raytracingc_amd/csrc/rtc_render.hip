@@ -159,6 +159,10 @@ struct RtcDeviceScene {
      * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
     unsigned char *scratch;
     size_t scratchCap; /* bytes */
+    /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
+     * sample order by rtc_accumulate_samples (grown on demand, <= kSampleBufBudget bytes) */
+    unsigned char *samples;
+    size_t samplesCap; /* bytes */
     int maskWords;     /* ceil(triPadded / 64) */
     unsigned long long *segSlots; /* per-launch partial segment counters */
     /* the split launch runs the sky kernel on `side`, concurrently with the heavy-tile kernel */
@@ -427,6 +431,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->primX);
     if (s->scratch)
         (void)hipFree(s->scratch);
+    if (s->samples)
+        (void)hipFree(s->samples);
     if (s->segSlots)
         (void)hipFree(s->segSlots);
     if (s->evFork)
@@ -475,6 +481,9 @@ struct RenderParams {
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
+    float4 *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
+    int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
+    int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
@@ -2318,6 +2327,7 @@ __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
  * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
  * Work: one wave per geometry pixel (rtc_pixel_list), statically strided over a fixed grid (no atomics). */
+constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
 constexpr int kChainBlock = 256;
 constexpr int kChainWorkers = 2048;
 #ifndef RTC_CHAIN_UNROLL
@@ -2463,6 +2473,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         for (int w = 0; w < P.maskWords; ++w)
             L += (unsigned)__popcll(mask[w]);
         const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
+        const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
             closest_primary_listed(P, pdir, prim, 0, mask);
@@ -2550,40 +2561,78 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
             DSECT_BEGIN(dc7);
-            const V3 t = mul(light, P.invSpp);
-            /* every lane's calcColor(...) * (float)(1./spp) into LDS (the ray slots are free now); the walk reads the
-             * members back with uniform (broadcast) LDS reads and adds them in sample order, x and y as one packed
-             * f32 add (two IEEE adds) */
-            W.ray[lane][0] = make_float4(t.x, t.y, t.z, 0.f);
-            wave_lds_sync();
+            const V3 t = mul(light, P.invSpp); /* calcColor(...) * (float)(1./spp), main.c:99 */
             const unsigned long long ones = __ballot(act && hits == 1u);
             unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
             int p = 0;
-            while (k < P.spp && p < nAct) {
-                const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
-                const unsigned long long notOne = ~ones & win;
-                const int q = notOne ? __builtin_ctzll(notOne) : nAct;
-                const int take = min(q - p, P.spp - k);
+            if (deferred) {
+                /* membership only: member lane b of sample index kk stores t at [item][kk]; rtc_accumulate_samples
+                 * adds them in sample order */
+                float4 *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+                const float4 tv = make_float4(t.x, t.y, t.z, 0.f);
+                while (k < P.spp && p < nAct) {
+                    const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
+                    const unsigned long long notOne = ~ones & win;
+                    const int q = notOne ? __builtin_ctzll(notOne) : nAct;
+                    const int take = min(q - p, P.spp - k);
+                    if (lane >= p && lane < p + take) {
+                        slot[k + lane - p] = tv;
+                        mult++;
+                    }
+                    k += take;
+                    p += take;
+                    if (k >= P.spp || p != q || q >= nAct)
+                        break;
+                    /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
+                    const int hq = __builtin_amdgcn_readlane((int)hits, q);
+                    if (hq == 0) { /* the primary ray misses: every remaining sample is this one (no draws) */
+                        const float4 vq = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q)),
+                                                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q)),
+                                                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q)), 0.f);
+                        for (int kk = k + lane; kk < P.spp; kk += 64)
+                            slot[kk] = vq;
+                        mult += lane == q ? (unsigned)(P.spp - k) : 0u;
+                        k = P.spp;
+                        break;
+                    }
+                    if (lane == q) {
+                        slot[k] = tv;
+                        mult++;
+                    }
+                    k++;
+                    p = q + hq;
+                }
+            } else {
+                /* the members are added here, in sample order: t from LDS (the ray slots are free now) with
+                 * uniform (broadcast) reads, x and y as one packed f32 add (two IEEE adds) */
+                W.ray[lane][0] = make_float4(t.x, t.y, t.z, 0.f);
+                wave_lds_sync();
+                while (k < P.spp && p < nAct) {
+                    const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
+                    const unsigned long long notOne = ~ones & win;
+                    const int q = notOne ? __builtin_ctzll(notOne) : nAct;
+                    const int take = min(q - p, P.spp - k);
 #pragma unroll 8
-                for (int b = p; b < p + take; ++b) { /* a run of one-hit samples: j advances by 1 */
-                    const float4 v = W.ray[b][0];
+                    for (int b = p; b < p + take; ++b) { /* a run of one-hit samples: j advances by 1 */
+                        const float4 v = W.ray[b][0];
+                        accxy = accxy + f2{v.x, v.y};
+                        accz = accz + v.z;
+                    }
+                    mult += (lane >= p && lane < p + take) ? 1u : 0u;
+                    k += take;
+                    p += take;
+                    if (k >= P.spp || p != q || q >= nAct)
+                        break;
+                    /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
+                    const float4 v = W.ray[q][0];
                     accxy = accxy + f2{v.x, v.y};
                     accz = accz + v.z;
+                    mult += lane == q ? 1u : 0u;
+                    k++;
+                    p = q + __builtin_amdgcn_readlane((int)hits, q);
                 }
-                mult += (lane >= p && lane < p + take) ? 1u : 0u;
-                k += take;
-                p += take;
-                if (k >= P.spp || p != q || q >= nAct)
-                    break;
-                /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
-                const float4 v = W.ray[q][0];
-                accxy = accxy + f2{v.x, v.y};
-                accz = accz + v.z;
-                mult += lane == q ? 1u : 0u;
-                k++;
-                p = q + __builtin_amdgcn_readlane((int)hits, q);
+                wave_lds_sync(); /* the ray slots are rewritten by the next round */
             }
-            wave_lds_sync(); /* the ray slots are rewritten by the next round */
             jn += (unsigned)p;
             /* counters: committed samples (with multiplicity) and the tests of the discarded ones */
             segCalls += (unsigned long long)mult * calls;
@@ -2594,7 +2643,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 segSpec += tests;
             DSECT_END(dc7, 7);
         }
-        if (lane == 0) {
+        if (deferred) {
+            if (lane == 0)
+                P.itemPix[it] = r * P.width + x;
+        } else if (lane == 0) {
             const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
             P.colors[3 * o] = float_to_u8(accxy.x);
             P.colors[3 * o + 1] = float_to_u8(accxy.y);
@@ -2611,6 +2663,39 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
 #endif
     flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
+}
+
+/* The deferred half of rtc_render_chain's walk: for each geometry pixel with a slot, its accumulated samples'
+ * radiance in sample order, added as the reference does (main.c:97-100: acc = acc + calcColor(...) * (1/spp),
+ * sequential f32 adds from 0), then vec3ToColor (raytracing.c:11-15).  One lane per pixel. */
+__global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
+{
+    int items = 0;
+    for (int l = 0; l < kGeoLists; ++l)
+        items += P.geoCount[l * kGeoCountStride];
+    items = min(items, P.sampleCap);
+    for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
+        const float4 *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+        f2 accxy{0.f, 0.f};
+        float accz = 0.f;
+        if (P.maxBounce > 0) {
+#pragma unroll 8
+            for (int k = 0; k < P.spp; ++k) {
+                const float4 v = slot[k];
+                accxy = accxy + f2{v.x, v.y};
+                accz = accz + v.z;
+            }
+        }
+        const size_t o = (size_t)P.itemPix[it];
+        P.colors[3 * o] = float_to_u8(accxy.x);
+        P.colors[3 * o + 1] = float_to_u8(accxy.y);
+        P.colors[3 * o + 2] = float_to_u8(accz);
+        if (P.accum) {
+            P.accum[3 * o] = accxy.x;
+            P.accum[3 * o + 1] = accxy.y;
+            P.accum[3 * o + 2] = accz;
+        }
+    }
 }
 
 /* ---- two samples in flight per pixel (rtc_render_pipe) ----------------------------------------------------
@@ -2974,6 +3059,25 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.geoCount = order + tiles + blocks + 4 + tiles * 64;
         P.geoList = P.geoCount + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
+        /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
+         * (pixels beyond it are accumulated inside rtc_render_chain; same result) */
+        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE)) {
+            const size_t per = (size_t)d->spp * sizeof(float4) + sizeof(int);
+            const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
+            const size_t need = cap * per + 256;
+            if (need > s->samplesCap) {
+                RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
+                if (ms->samples)
+                    HIP_TRY(hipFree(ms->samples));
+                ms->samples = nullptr;
+                ms->samplesCap = 0;
+                HIP_TRY(hipMalloc(&ms->samples, need));
+                ms->samplesCap = need;
+            }
+            P.sampleBuf = (float4 *)s->samples;
+            P.itemPix = (int *)(s->samples + cap * (size_t)d->spp * sizeof(float4));
+            P.sampleCap = (int)cap;
+        }
     }
     if (s->triPadded > 0 || chain)
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
@@ -3020,9 +3124,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
             const bool eight = forced == RTC_F_COOP8;
             const bool pipe = forced == RTC_F_PIPE;
-            if (chain)
+            if (chain) {
                 hipLaunchKernelGGL(rtc_render_chain, dim3(kChainWorkers), dim3(kChainBlock),
                                    (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
+                if (P.sampleCap > 0) {
+                    HIP_TRY(hipGetLastError());
+                    const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
+                    hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
+                }
+            }
             else if (spec)
                 hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
             else if (pipe)

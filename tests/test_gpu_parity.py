@@ -178,6 +178,11 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
     assert tests[0] == tests[1]
     if sph is None or len(sph) == 0:
         assert s1["tri_tests"] == tests[0] and s4["tri_tests"] == tests[0]
+    # the state-indexed kernel summing each pixel's samples itself (RTC_F_CHAIN_INLINE) == the deferred pass
+    c6, a6, s6 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "chain_inline": True}),
+                           want_accum=True)
+    assert np.array_equal(_bits(a1), _bits(a6)) and np.array_equal(c1, c6) and s1["segments"] == s6["segments"]
+    assert s6["tri_tests"] == s1["tri_tests"]
     if not hoist:
         c5, a5, s5 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "pipe": True}),
                                want_accum=True)
@@ -328,7 +333,7 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
 
 
 @pytest.mark.parametrize("variant", [{}, {"coop_lanes": 4}, {"coop_lanes": 8}, {"spec": True}, {"hoist": True},
-                                     {"pipe": True}])
+                                     {"pipe": True}, {"chain_inline": True}, {"hoist": True, "chain_inline": True}])
 def test_spp_not_multiple_of_64(variant, gpu_available):
     """spp = 100 (the speculative kernel's two rounds of 64 and 36 samples, the cooperative kernels' chains)
     against the oracle, bit for bit, with identical segment counts."""
