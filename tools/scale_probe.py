@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""One rank's share of the 1080p x64 ultracomplex frame at N GPUs (rows y = r + kN), rendered on one GPU:
-the per-rank device time that bounds strong scaling.  Not part of the product.
-Usage: scale_probe.py [frames] [lib-suffix]"""
+"""One rank's share of a frame at N GPUs (rows y = r + kN), rendered on one GPU: the per-rank device time that
+bounds strong scaling (the gather of the uint8 parts and the re-interleave come on top).  Not part of the product.
+Usage: scale_probe.py [frames] [W H spp] [kernel: chain|pipe|coop4]"""
 import json
 import os
 import sys
@@ -14,33 +14,39 @@ import torch  # noqa: E402
 import raytracingc_amd as rt  # noqa: E402
 from conftest import load_tris  # noqa: E402
 
-frames = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+frames = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
+kernel = sys.argv[5] if len(sys.argv) > 5 else "chain"
+extra = {"chain": {}, "pipe": {"pipe": True}, "coop4": {"coop_lanes": 4}}[kernel]
 tris, _ = load_tris("ultracomplex")
 scene, cam = rt.default_scene(), rt.camera_basis()
-W, H, SPP = 1920, 1080, 64
 ds = rt.DeviceScene(tris, None)
-ds.set_timing(True)
 stream = torch.cuda.current_stream()
 out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
+for _ in range(20):  # clocks settle
+    ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, SPP, 10, True, **extra), out.data_ptr(), None, None,
+                         stream.cuda_stream)
+torch.cuda.synchronize()
 base = None
 for n in (1, 2, 4, 8):
-    for r, lanes in [(0, 0), (0, -1)]:
-        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, pipe=(lanes == 0))
-        times, kts = [], []
+    worst = 0.0
+    per = []
+    for r in range(n):  # every rank's share: the slowest sets the frame
+        cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, **extra)
+        times = []
         for _ in range(frames):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
+            ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, None, stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))
-            kts.append(ds.kernel_times())
         ms = sorted(times)[len(times) // 2]
-        if n == 1 and base is None:
-            base = ms
-        heavy = sorted(k[0] for k in kts if k)[len(kts) // 2] if any(kts) else None
-        print(json.dumps({"n": n, "rank": r, "kernel": "pipe" if lanes == 0 else "coop", "ms_median": round(ms, 3), "heavy_ms": round(heavy, 3) if heavy else None,
-                          "ideal_ms": round(base / n, 3), "efficiency_if_only_this": round(base / n / ms, 3)}),
-              flush=True)
+        per.append(round(ms, 4))
+        worst = max(worst, ms)
+    if base is None:
+        base = worst
+    print(json.dumps({"n": n, "W": W, "H": H, "spp": SPP, "kernel": kernel, "rank_ms": per, "slowest_ms": round(worst, 4),
+                      "ideal_ms": round(base / n, 4), "speedup_bound": round(base / worst, 3),
+                      "efficiency_bound": round(base / n / worst, 3)}), flush=True)
 ds.close()
