@@ -184,9 +184,10 @@ int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *
 int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
                      vec3 *direction);                                                                  /* moremath.c:89-108 */
 /* Soundness probe of the bounce-ray cluster culling (no reference counterpart; raytracing.c:186-214 is the
- * per-triangle test it must never contradict): clusters `tris` as rtc_scene_upload does and, for every ray,
- * counts [0] hits inside clusters the ray was culled from (0 when sound), [1] clusters culled, [2] cluster
- * tests, [3] hits, [4] float bits of the largest hit-point excess over a cluster's bounding radius. */
+ * per-triangle test it must never contradict): clusters `tris` as rtc_scene_upload does and, for every ray and
+ * every cluster ball (8 triangles) and chunk ball (32 clusters, scenes of more than one chunk), counts [0] hits
+ * inside balls the ray was culled from (0 when sound), [1] balls culled, [2] ball tests, [3] hits, [4] float
+ * bits of the largest hit-point excess over a ball's radius. */
 int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
                             unsigned long long counts[5]);
 

@@ -137,6 +137,7 @@ struct __attribute__((aligned(64))) DevPrimX {
  * safety factor F = 4; gamma covers the f32 evaluation of the cull test itself).  Clusters with
  * 8 u E^2 rhoMax / EPSILON >= 1/2, and rays with |dir|_1 > rhoMax, are never culled. */
 constexpr int kClusterSize = 8;
+constexpr int kChunkClusters = 32; /* clusters per chunk (one 32-bit cull mask per lane in rtc_render_chain) */
 constexpr float kClusterRhoMax = 4.f;
 constexpr float kClusterGamma = 2e-5f;
 struct __attribute__((aligned(32))) DevCluster {
@@ -150,6 +151,8 @@ struct RtcDeviceScene {
     int clusterCount;   /* ceil(triCount / kClusterSize) */
     DevTri *clTris;     /* clusterCount * kClusterSize records in cluster order, pad0 = reference index (int) */
     DevCluster *clusters;
+    DevCluster *chunks; /* chunkCount balls over kChunkClusters consecutive clusters */
+    int chunkCount;
     DevTri *tris;
     DevMat *mats;
     DevSphere *spheres;
@@ -257,8 +260,77 @@ static void split_clusters(const std::vector<DevTri> &dt, std::vector<int> &idx,
     split_clusters(dt, idx, mid, hi);
 }
 
+/* Bounding ball and cull margins (DevCluster) of the records ct[first, first + count) whose index (pad0) is
+ * >= 0: the ball holds every vertex A, A + AB, A + AC; E is the longest AB / AC edge. */
+static DevCluster ball_of(const std::vector<DevTri> &ct, size_t first, size_t count)
+{
+    const double u = 0x1p-24, eps = 0.001; /* |det| >= 0.001f > 0.001 for every reported hit */
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, E = 0.0;
+    bool finite = true;
+    int n = 0;
+    auto real = [&](const DevTri &r) {
+        int i;
+        memcpy(&i, &r.pad0, sizeof i);
+        return i >= 0;
+    };
+    for (size_t j = first; j < first + count; ++j) {
+        const DevTri &r = ct[j];
+        if (!real(r))
+            continue;
+        ++n;
+        const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
+        for (int a = 0; a < 3; ++a) {
+            const double v[3] = {A[a], A[a] + B[a], A[a] + C[a]};
+            for (double x : v) {
+                finite = finite && std::isfinite(x);
+                lo[a] = std::min(lo[a], x);
+                hi[a] = std::max(hi[a], x);
+            }
+        }
+        E = std::max(E, std::max(std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]),
+                                 std::sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2])));
+    }
+    DevCluster k{};
+    const double ctr[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
+    k.cx = n ? (float)ctr[0] : 0.f;
+    k.cy = n ? (float)ctr[1] : 0.f;
+    k.cz = n ? (float)ctr[2] : 0.f;
+    double R = 0.0;
+    for (size_t j = first; j < first + count; ++j) { /* radius about the rounded (float) centre */
+        const DevTri &r = ct[j];
+        if (!real(r))
+            continue;
+        const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
+        const double K[3] = {k.cx, k.cy, k.cz};
+        for (int w = 0; w < 3; ++w) {
+            double d2 = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                const double x = A[a] + (w == 1 ? B[a] : w == 2 ? C[a] : 0.0) - K[a];
+                d2 += x * x;
+            }
+            R = std::max(R, std::sqrt(d2));
+        }
+    }
+    const double F = 4.0, edRatio = 8.0 * u * E * E * kClusterRhoMax / eps;
+    k.r = std::nextafter((float)(R * (1.0 + 1e-9)), INFINITY);
+    k.e = (float)E;
+    if (!finite || n == 0 || !(edRatio < 0.5) || !(k.r < 1e18f)) {
+        k.alpha = INFINITY; /* never culled */
+        k.beta = k.gammaE = 0.f;
+        return k;
+    }
+    const double kk = 1.0 / (1.0 - edRatio);
+    k.alpha = std::nextafter((float)(F * kk * 32.0 * u * E * E * E / eps), INFINITY);
+    k.beta = std::nextafter((float)(F * kk * 45.0 * u * E * E / eps), INFINITY);
+    k.gammaE = std::nextafter((float)(kClusterGamma * E), INFINITY);
+    return k;
+}
+
+/* ct: the records in cluster order (pad0 = reference index, -1 for padding), cl: one ball per cluster of
+ * kClusterSize, ch: one ball per chunk of kChunkClusters consecutive clusters (a subtree of the median split:
+ * the chain kernel's first culling level for scenes of more than one chunk) */
 static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std::vector<DevTri> &ct,
-                               std::vector<DevCluster> &cl)
+                               std::vector<DevCluster> &cl, std::vector<DevCluster> &ch)
 {
     const int nc = (triCount + kClusterSize - 1) / kClusterSize;
     std::vector<int> idx(triCount);
@@ -267,10 +339,7 @@ static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std:
     split_clusters(dt, idx, 0, (size_t)triCount);
     ct.assign((size_t)nc * kClusterSize, DevTri{});
     cl.assign((size_t)(nc > 0 ? nc : 1), DevCluster{});
-    const double u = 0x1p-24, eps = 0.001; /* |det| >= 0.001f > 0.001 for every reported hit */
     for (int c = 0; c < nc; ++c) {
-        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, E = 0.0;
-        bool finite = true;
         const int n = std::min(kClusterSize, triCount - c * kClusterSize);
         for (int j = 0; j < kClusterSize; ++j) {
             DevTri &r = ct[(size_t)c * kClusterSize + j];
@@ -282,49 +351,14 @@ static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std:
             const int i = idx[(size_t)c * kClusterSize + j];
             r = dt[i];
             memcpy(&r.pad0, &i, sizeof i);
-            const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
-            for (int a = 0; a < 3; ++a) {
-                const double v[3] = {A[a], A[a] + B[a], A[a] + C[a]};
-                for (double x : v) {
-                    finite = finite && std::isfinite(x);
-                    lo[a] = std::min(lo[a], x);
-                    hi[a] = std::max(hi[a], x);
-                }
-            }
-            E = std::max(E, std::max(std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]),
-                                     std::sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2])));
         }
-        DevCluster &k = cl[c];
-        const double ctr[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
-        k.cx = (float)ctr[0];
-        k.cy = (float)ctr[1];
-        k.cz = (float)ctr[2];
-        double R = 0.0;
-        for (int j = 0; j < n; ++j) { /* radius about the rounded (float) centre */
-            const DevTri &r = ct[(size_t)c * kClusterSize + j];
-            const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
-            const double K[3] = {k.cx, k.cy, k.cz};
-            for (int w = 0; w < 3; ++w) {
-                double d2 = 0.0;
-                for (int a = 0; a < 3; ++a) {
-                    const double x = A[a] + (w == 1 ? B[a] : w == 2 ? C[a] : 0.0) - K[a];
-                    d2 += x * x;
-                }
-                R = std::max(R, std::sqrt(d2));
-            }
-        }
-        const double F = 4.0, edRatio = 8.0 * u * E * E * kClusterRhoMax / eps;
-        k.r = std::nextafter((float)(R * (1.0 + 1e-9)), INFINITY);
-        k.e = (float)E;
-        if (!finite || n == 0 || !(edRatio < 0.5) || !(k.r < 1e18f)) {
-            k.alpha = INFINITY; /* never culled */
-            k.beta = k.gammaE = 0.f;
-            continue;
-        }
-        const double kk = 1.0 / (1.0 - edRatio);
-        k.alpha = std::nextafter((float)(F * kk * 32.0 * u * E * E * E / eps), INFINITY);
-        k.beta = std::nextafter((float)(F * kk * 45.0 * u * E * E / eps), INFINITY);
-        k.gammaE = std::nextafter((float)(kClusterGamma * E), INFINITY);
+        cl[c] = ball_of(ct, (size_t)c * kClusterSize, kClusterSize);
+    }
+    const int nch = (nc + kChunkClusters - 1) / kChunkClusters;
+    ch.assign((size_t)(nch > 0 ? nch : 1), DevCluster{});
+    for (int h = 0; h < nch; ++h) {
+        const size_t c0 = (size_t)h * kChunkClusters, c1 = std::min<size_t>((size_t)nc, c0 + kChunkClusters);
+        ch[h] = ball_of(ct, c0 * kClusterSize, (c1 - c0) * kClusterSize);
     }
 }
 
@@ -350,8 +384,8 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     std::vector<DevSphere> ds;
     pack_scene(tris, triCount, spheres, sphereCount, dt, dm, ds);
     std::vector<DevTri> ct;
-    std::vector<DevCluster> cl;
-    rtc_build_clusters(dt, triCount, ct, cl);
+    std::vector<DevCluster> cl, ch;
+    rtc_build_clusters(dt, triCount, ct, cl, ch);
     if (ct.empty())
         ct.assign(1, DevTri{});
     RtcDeviceScene *s = new RtcDeviceScene();
@@ -361,6 +395,7 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     s->sphereCount = sphereCount;
     s->maskWords = (s->triPadded + 63) / 64;
     s->clusterCount = (triCount + kClusterSize - 1) / kClusterSize;
+    s->chunkCount = (s->clusterCount + kChunkClusters - 1) / kChunkClusters;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
     if (e == hipSuccess)
         e = hipMalloc(&s->clTris, ct.size() * sizeof(DevTri));
@@ -370,6 +405,10 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipMemcpy(s->clTris, ct.data(), ct.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->clusters, cl.data(), cl.size() * sizeof(DevCluster), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMalloc(&s->chunks, ch.size() * sizeof(DevCluster));
+    if (e == hipSuccess)
+        e = hipMemcpy(s->chunks, ch.data(), ch.size() * sizeof(DevCluster), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
     if (e == hipSuccess)
@@ -421,6 +460,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->clTris);
     if (s->clusters)
         (void)hipFree(s->clusters);
+    if (s->chunks)
+        (void)hipFree(s->chunks);
     if (s->mats)
         (void)hipFree(s->mats);
     if (s->spheres)
@@ -466,6 +507,8 @@ struct RenderParams {
     const DevPrimX *__restrict__ primX;
     const DevTri *__restrict__ clTris;         /* cluster order (rtc_build_clusters) */
     const DevCluster *__restrict__ clusters;
+    const DevCluster *__restrict__ chunks;
+    int chunkCount;
     int clusterCount, clusterCull;
     const unsigned long long *__restrict__ tileMask; /* null: primary segments test every triangle */
     const unsigned long long *__restrict__ pixMask;  /* per 8x8 tile: pixels with a primary candidate (bit i =
@@ -2355,7 +2398,7 @@ struct ChainWaveLds {
     unsigned short pair[64 * 32]; /* lane | cluster << 6, cluster-major */
 };
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
-static_assert(kCoopMaxTris / kClusterSize <= 32, "the pair list holds 32 clusters per lane");
+static_assert(kChunkClusters <= 32, "the pair list holds one chunk of clusters per lane");
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -2364,6 +2407,7 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <bool MULTI>
 __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, V3 pos, V3 dir,
                                                      const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
                                                      unsigned &tests)
@@ -2371,74 +2415,94 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     W.ray[lane][0] = make_float4(pos.x, pos.y, pos.z, 0.f);
     W.ray[lane][1] = make_float4(dir.x, dir.y, dir.z, 0.f);
     W.key[lane] = kNoHitKey;
-    unsigned cm = 0;
-    DSECT_BEGIN(dc3);
-    if (alive) {
-        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
-        const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
-        for (int k = 0; k < P.clusterCount; ++k)
-            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[k])) << k;
-        tests = (unsigned)__popc(cm) * kClusterSize -
-                ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
-    }
-    DSECT_END(dc3, 3);
-    DSECT_BEGIN(dc4);
-    int n = 0;
-    for (int k = 0; k < P.clusterCount; ++k) {
-        const unsigned long long m = __ballot((cm >> k) & 1u);
-        if ((cm >> k) & 1u)
-            W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
-                (unsigned short)(lane | (k << 6));
-        n += (int)__popcll(m);
-    }
-    wave_lds_sync();
-    DSECT_END(dc4, 4);
-    DSECT_BEGIN(dc5);
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
-        if (i < n) {
-            const unsigned pr = W.pair[i];
-            const int o = (int)(pr & 63u), k = (int)(pr >> 6);
-            const float4 rp = W.ray[o][0], rd = W.ray[o][1];
-            const V3 rpos{rp.x, rp.y, rp.z}, rdir{rd.x, rd.y, rd.z};
-            const DevTri *R = sRec + k * kClusterSize;
-            unsigned surv = 0;
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
+    tests = 0;
+    /* scenes of more than kChunkClusters clusters: chunk by chunk (a chunk's ball culls its clusters for a lane
+     * at once); the records come from global memory when they are not staged in LDS (sRec null) */
+    const int nChunks = MULTI ? P.chunkCount : 1;
+    for (int h = 0; h < nChunks; ++h) {
+        const int c0 = h * kChunkClusters, nCl = MULTI ? min(kChunkClusters, P.clusterCount - c0) : P.clusterCount;
+        bool in = alive;
+        if (MULTI) {
+            if (alive)
+                in = !(rhoOk && cluster_culled(pos, dir, rho, P.chunks[h]));
+            if (!__ballot(in))
+                continue;
+        }
+        unsigned cm = 0;
+        DSECT_BEGIN(dc3);
+        if (in) {
+            for (int k = 0; k < nCl; ++k)
+                cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[c0 + k])) << k;
+            /* triangles in the clusters kept (only the scene's last cluster has zero records) */
+            tests += (unsigned)__popc(cm) * kClusterSize -
+                     (c0 + nCl == P.clusterCount ? ((cm >> (nCl - 1)) & 1u) : 0u) *
+                         (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+        }
+        DSECT_END(dc3, 3);
+        DSECT_BEGIN(dc4);
+        int n = 0;
+        for (int k = 0; k < nCl; ++k) {
+            const unsigned long long m = __ballot((cm >> k) & 1u);
+            if ((cm >> k) & 1u)
+                W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                    (unsigned short)(lane | (k << 6));
+            n += (int)__popcll(m);
+        }
+        wave_lds_sync();
+        DSECT_END(dc4, 4);
+        DSECT_BEGIN(dc5);
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + lane;
+            if (i < n) {
+                const unsigned pr = W.pair[i];
+                const int o = (int)(pr & 63u), k = c0 + (int)(pr >> 6);
+                const float4 rp = W.ray[o][0], rd = W.ray[o][1];
+                const V3 rpos{rp.x, rp.y, rp.z}, rdir{rd.x, rd.y, rd.z};
+                const DevTri *R = (MULTI ? P.clTris : sRec) + k * kClusterSize;
+                unsigned surv = 0;
 #pragma unroll RTC_CHAIN_UNROLL
-            for (int j = 0; j < kClusterSize; ++j)
-                surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
-            if (surv) {
-                Closest c{999999.f, -1};
-                while (surv) {
-                    const int j = __builtin_ctz(surv);
-                    surv &= surv - 1;
-                    general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
+                for (int j = 0; j < kClusterSize; ++j)
+                    surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
+                if (surv) {
+                    Closest c{999999.f, -1};
+                    while (surv) {
+                        const int j = __builtin_ctz(surv);
+                        surv &= surv - 1;
+                        general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
+                    }
+                    if (c.idx >= 0 && c.dst < 999999.f)
+                        atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
                 }
-                if (c.idx >= 0 && c.dst < 999999.f)
-                    atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
             }
         }
+        wave_lds_sync(); /* the pair list is rewritten by the next chunk */
+        DSECT_END(dc5, 5);
     }
-    wave_lds_sync();
     const unsigned long long key = W.key[lane];
     Closest c{999999.f, -1};
     if (key != kNoHitKey) {
         c.dst = __uint_as_float((unsigned)(key >> 32));
         c.idx = (int)(unsigned)key;
     }
-    DSECT_END(dc5, 5);
     return c;
 }
 
+template <bool MULTI> /* more than one chunk of clusters: chunk-level culling, records from global memory */
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
-    DevTri *sRec = (DevTri *)sDyn; /* the clustered scene records (clusterCount * 8; pad0 = reference index) */
+    /* the clustered scene records (clusterCount * 8; pad0 = reference index), staged in LDS up to one chunk */
+    DevTri *sRec = MULTI ? nullptr : (DevTri *)sDyn;
     sPow.fill(threadIdx.x);
-    for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
-        sRec[i] = P.clTris[i];
+    if (!MULTI)
+        for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
+            sRec[i] = P.clTris[i];
 #ifdef RTC_DIAG
     if ((threadIdx.x & 63) < 8)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
@@ -2516,7 +2580,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     DSECT_END(dc1, 1);
                 } else { /* bounce segments of the live lanes (the whole wave takes part) */
                     unsigned t = 0;
-                    c = chain_trace_pairs(P, alive, pos, dir, sRec, W, lane, t);
+                    c = chain_trace_pairs<MULTI>(P, alive, pos, dir, sRec, W, lane, t);
                     if (alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
@@ -2990,6 +3054,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.triPadded = s->triPadded;
     P.clTris = s->clTris;
     P.clusters = s->clusters;
+    P.chunks = s->chunks;
+    P.chunkCount = s->chunkCount;
     P.clusterCount = s->clusterCount;
     P.clusterCull = !(d->flags & RTC_F_NO_CLUSTER_CULL);
     P.sphereCount = d->trianglesOnly ? 0 : s->sphereCount;
@@ -3019,7 +3085,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     /* (a scene without triangles culls too: every tile is then a sky tile) */
     const bool cull = !(d->flags & RTC_F_NO_TILE_CULL);
-    const bool fused = cull && !debug && P.sphereCount == 0 && s->triPadded <= kCoopMaxTris &&
+    /* the split launch: every scene for rtc_render_chain, up to kCoopMaxTris triangles for the older heavy
+     * kernels (their scene records live in LDS) */
+    const int forcedHeavy = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
+    const bool fused = cull && !debug && P.sphereCount == 0 && (forcedHeavy == 0 || s->triPadded <= kCoopMaxTris) &&
                        !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
@@ -3125,8 +3194,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const bool eight = forced == RTC_F_COOP8;
             const bool pipe = forced == RTC_F_PIPE;
             if (chain) {
-                hipLaunchKernelGGL(rtc_render_chain, dim3(kChainWorkers), dim3(kChainBlock),
-                                   (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
+                if (s->chunkCount <= 1)
+                    hipLaunchKernelGGL(rtc_render_chain<false>, dim3(kChainWorkers), dim3(kChainBlock),
+                                       (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
+                else
+                    hipLaunchKernelGGL(rtc_render_chain<true>, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
                 if (P.sampleCap > 0) {
                     HIP_TRY(hipGetLastError());
                     const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
@@ -3266,8 +3338,8 @@ __global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, 
  * every triangle of the cluster is tested with the reference's rayTriangle arithmetic.  counts: [0] hits in
  * culled clusters (must stay 0), [1] clusters culled, [2] cluster tests, [3] hits, [4] float bits of the
  * largest (distance from the ball centre to the reported hit point) - r over all hits. */
-__global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl, int clusterCount, const Ray *rays,
-                                     size_t n, unsigned long long *counts)
+__global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl, int clusterCount, int per,
+                                     int recCount, const Ray *rays, size_t n, unsigned long long *counts)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n)
@@ -3280,8 +3352,8 @@ __global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl,
         const DevCluster K = cl[k];
         const bool cut = rho <= kClusterRhoMax && cluster_culled(pos, dir, rho, K);
         culled += cut;
-        for (int j = 0; j < kClusterSize; ++j) {
-            const DevTri R = clTris[k * kClusterSize + j];
+        for (int j = 0; j < per && k * per + j < recCount; ++j) {
+            const DevTri R = clTris[k * per + j];
             if (__float_as_int(R.pad0) < 0)
                 continue;
             float dst;
@@ -3448,9 +3520,15 @@ extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const
     if (e == hipSuccess)
         e = hipMemset(dc, 0, 5 * sizeof(unsigned long long));
     if (e == hipSuccess) {
+        /* the clusters, then the chunks (balls over kChunkClusters clusters, rtc_render_chain's first level) */
         hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->clusters,
-                           s->clusterCount, dr, n, dc);
+                           s->clusterCount, kClusterSize, s->clusterCount * kClusterSize, dr, n, dc);
         e = hipGetLastError();
+        if (e == hipSuccess && s->chunkCount > 1) {
+            hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->chunks,
+                               s->chunkCount, kClusterSize * kChunkClusters, s->clusterCount * kClusterSize, dr, n, dc);
+            e = hipGetLastError();
+        }
     }
     if (e == hipSuccess)
         e = hipMemcpy(counts, dc, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);

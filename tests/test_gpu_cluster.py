@@ -105,12 +105,13 @@ def _scaled(tris, s):
 
 @pytest.mark.parametrize("name,scale", [("ultracomplex", 1.0), ("complex", 1.0), ("cube", 1.0),
                                         ("ultracomplex", 40.0), ("ultracomplex", 0.02), ("fsuzane", 1.0),
-                                        ("4geoms", 1.0), ("default", 1.0)])
+                                        ("4geoms", 1.0), ("default", 1.0), ("suzannes", 1.0), ("suzannes", 25.0)])
 def test_cluster_culling_is_sound(name, scale, gpu_available):
+    """suzannes.obj (5,208 triangles, 21 chunks) also checks the chunk balls of rtc_render_chain's first level."""
     tris, _ = load_tris(name)
     tris = _scaled(tris, scale)
     rng = np.random.default_rng(1234 + int(scale * 100))
-    rays = _rays(tris, 250_000, rng)
+    rays = _rays(tris, 250_000 if len(tris) <= 256 else 40_000, rng)
     r = rt.cluster_bound_probe(tris, rays)
     print(name, scale, r)
     assert r["violations"] == 0, r

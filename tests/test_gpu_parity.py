@@ -444,9 +444,10 @@ def test_full_size_baseline_configs(scene, W, H, spp, row0, stride, gpu_availabl
 
 
 @pytest.mark.parametrize("name", ["suzannes_96x54x4", "suzannes_cam_64x48x2"])
-def test_large_scene_general_kernel(name, gpu_available):
-    """suzannes.obj (5,208 triangles, T > 256: the general kernel) against the reference's golden hash, and
-    tile culling == brute force on it."""
+def test_large_scene(name, gpu_available):
+    """suzannes.obj (5,208 triangles = 651 clusters in 21 chunks: rtc_render_chain with records from global
+    memory and chunk-level culling) against the reference's golden hash; == the one-lane-per-pixel kernel with
+    and without tile culling, bit for bit, with the same segment counts."""
     g = GOLD[name]
     tris, tonly = load_tris(g["scene"])
     assert len(tris) > 256
@@ -454,9 +455,21 @@ def test_large_scene_general_kernel(name, gpu_available):
     base = rt.RenderConfig(g["width"], g["height"], g["spp"], mb, bool(tonly))
     c1, a1, s1 = rt.render(tris, None, scene, cam, base, want_accum=True)
     assert hashlib.sha256(a1.tobytes()).hexdigest() == g["float_sha256"]
-    c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**base.__dict__, "tile_cull": False}),
-                           want_accum=True)
-    assert np.array_equal(_bits(a0), _bits(a1)) and s0["segments"] == s1["segments"]
+    for kw in ({"tile_cull": False}, {"coop": False}, {"chain_inline": True}, {"hoist": True}):
+        c0, a0, s0 = rt.render(tris, None, scene, cam, rt.RenderConfig(**{**base.__dict__, **kw}), want_accum=True)
+        assert np.array_equal(_bits(a0), _bits(a1)) and np.array_equal(c0, c1) and s0["segments"] == s1["segments"], kw
+
+
+def test_large_scene_full_frame(gpu_available):
+    """suzannes.obj at 640x360x16 through rtc_render_chain vs the oracle on a row sample, bit for bit."""
+    tris, tonly = load_tris("suzannes")
+    scene, cam, _ = setup_from_flags({})
+    W, H, spp = 640, 360, 16
+    c1, a1, s1 = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True), want_accum=True)
+    d = RtcRenderDesc(W, H, spp, 10, tonly, 1, 9, 0)
+    ocol, oacc, oseg = orc.render(tris, None, scene, cam, d, threads=16)
+    assert np.array_equal(_bits(a1[1::9]), _bits(oacc)) and np.array_equal(c1[1::9], ocol)
+    print(f"suzannes {W}x{H}x{spp}: render {s1['render_ms']:.3f} ms")
 
 
 def test_edge_sizes(gpu_available):
