@@ -1545,18 +1545,41 @@ __global__ __launch_bounds__(1024) void rtc_order_heavy(const unsigned *__restri
 
 
 /* True when the bounce ray (pos, dir) provably cannot hit any triangle of cluster K (see DevCluster): the
- * half-line's distance to the ball centre exceeds r + eps.  rho = |dir|_1 >= |dir|; NaN never culls. */
-__device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, const DevCluster &K)
+ * half-line's distance to the ball centre exceeds T >= r + eps.  rho = |dir|_1 >= |dir| bounds the eps terms;
+ * dd = dir.dir.  With w = centre - pos and b = w.dir, the half-line's closest point to the centre is interior
+ * when b > 0, at distance |w x dir| / |dir|, else the origin, at |w|.  |w x dir|^2 is evaluated by Lagrange's
+ * identity w2 dd - b^2 (FMA dots, each within 3u relative; the cancellation is covered by an explicit margin of
+ * 25u w2 dd >= the evaluation error) and compared with T^2 dd: the 1.00001 factor on T covers dd's own error.
+ * The f32 evaluation of w, S and T is covered by the gamma terms (rtc_build_clusters).  NaN never culls.
+ * cluster_terms: the per-(origin, cluster) values, culled_by: the per-direction test (the chain kernel tabulates
+ * the first for a pixel's primary hit point, where every first bounce starts). */
+struct ClusterTerms {
+    V3 w;
+    float w2, A, B; /* T = (A + rho B) * 1.00001 */
+};
+__device__ __forceinline__ ClusterTerms cluster_terms(V3 pos, const DevCluster &K)
 {
-    const V3 w = sub(V3{K.cx, K.cy, K.cz}, pos);
-    const float S = fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + K.r; /* >= |pos - A| for every vertex A */
-    const float T = (K.r + rho * (K.alpha + K.beta * S) + kClusterGamma * S + K.gammaE) * 1.00001f;
+    ClusterTerms t;
+    t.w = sub(V3{K.cx, K.cy, K.cz}, pos);
+    const float S = fabsf(t.w.x) + fabsf(t.w.y) + fabsf(t.w.z) + K.r; /* >= |pos - A| for every vertex A */
+    t.w2 = fmaf(t.w.z, t.w.z, fmaf(t.w.y, t.w.y, t.w.x * t.w.x));
+    t.A = (K.r + kClusterGamma * S) + K.gammaE;
+    t.B = fmaf(K.beta, S, K.alpha);
+    return t;
+}
+__device__ __forceinline__ bool culled_by(const ClusterTerms &t, V3 dir, float rho, float dd)
+{
+    const float T = fmaf(rho, t.B, t.A) * 1.00001f;
     const float T2 = T * T;
-    const float b = dot(w, dir);
-    const V3 x = cross(w, dir);
-    const float x2 = dot(x, x), w2 = dot(w, w);
-    /* b > 0: the closest point is interior, distance |w x dir| / |dir| >= sqrt(x2) / rho; else the origin */
-    return b > 0.f ? x2 > T2 * (rho * rho) : w2 > T2;
+    const float b = fmaf(t.w.z, dir.z, fmaf(t.w.y, dir.y, t.w.x * dir.x));
+    const float wd = t.w2 * dd;
+    const float x2 = fmaf(-b, b, wd);
+    return b > 0.f ? (x2 - 1.5e-6f * wd > T2 * dd) : (t.w2 > T2);
+}
+__device__ __forceinline__ float dir_dd(V3 dir) { return fmaf(dir.z, dir.z, fmaf(dir.y, dir.y, dir.x * dir.x)); }
+__device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, float dd, const DevCluster &K)
+{
+    return culled_by(cluster_terms(pos, K), dir, rho, dd);
 }
 
 /* In-group lane exchanges by DPP (VALU lane moves, no LDS round trip; ds_bpermute costs a wait of ~100
@@ -1663,11 +1686,11 @@ __device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 
          * the group), then the records of those clusters, lane sub taking records sub, sub+KC, ... of each;
          * survivor bit = cluster * kPer + j.  sTri holds the records in cluster order (pad0 = index). */
         constexpr int kPer = kClusterSize / KC;
-        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
         const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
         unsigned cm = 0;
         for (int k = sub; k < P.clusterCount; k += KC)
-            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, sCl[k])) << k;
+            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, dd, sCl[k])) << k;
         cm = group_or<KC>(cm);
         /* triangles in the clusters kept (only the last cluster has zero records) */
         testedTris = (unsigned)__popc(cm) * kClusterSize -
@@ -2152,10 +2175,10 @@ __device__ __forceinline__ Closest trace_clusters(const RenderParams &P, V3 pos,
                                                   const DevCluster *__restrict__ sCl, unsigned &tests)
 {
     Closest c{999999.f, -1};
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
     const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
     for (int k = 0; k < P.clusterCount; ++k) {
-        if (rhoOk && cluster_culled(pos, dir, rho, sCl[k]))
+        if (rhoOk && cluster_culled(pos, dir, rho, dd, sCl[k]))
             continue;
         tests += (unsigned)min(kClusterSize, P.triCount - k * kClusterSize);
         unsigned surv = 0;
@@ -2394,6 +2417,7 @@ constexpr int kChainWorkers = 2048;
 typedef float f2 __attribute__((ext_vector_type(2)));
 struct ChainWaveLds {
     float4 ray[64][2];            /* pos, dir of each lane's segment */
+    float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
     unsigned short pair[64 * 32]; /* lane | cluster << 6, cluster-major */
 };
@@ -2408,16 +2432,30 @@ __device__ __forceinline__ void wave_lds_sync()
 }
 
 template <bool MULTI>
-__device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, V3 pos, V3 dir,
-                                                     const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
-                                                     unsigned &tests)
+__device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, bool firstBounce, V3 pos,
+                                                     V3 dir, const DevTri *__restrict__ sRec, ChainWaveLds &W,
+                                                     int lane, unsigned &tests)
 {
     W.ray[lane][0] = make_float4(pos.x, pos.y, pos.z, 0.f);
     W.ray[lane][1] = make_float4(dir.x, dir.y, dir.z, 0.f);
     W.key[lane] = kNoHitKey;
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
+    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
     const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
     tests = 0;
+    /* a pixel's first bounces all start at its primary hit point (lane 0's pos): the clusters' origin terms
+     * once, one lane per cluster, into LDS (single-chunk scenes) */
+    const bool table = !MULTI && firstBounce;
+    if (table) {
+        const V3 p0{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.x), 0)),
+                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.y), 0)),
+                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.z), 0))};
+        if (lane < P.clusterCount) {
+            const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
+            W.cl[lane][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
+            W.cl[lane][1] = make_float4(t.A, t.B, 0.f, 0.f);
+        }
+        wave_lds_sync();
+    }
     /* scenes of more than kChunkClusters clusters: chunk by chunk (a chunk's ball culls its clusters for a lane
      * at once); the records come from global memory when they are not staged in LDS (sRec null) */
     const int nChunks = MULTI ? P.chunkCount : 1;
@@ -2426,15 +2464,23 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         bool in = alive;
         if (MULTI) {
             if (alive)
-                in = !(rhoOk && cluster_culled(pos, dir, rho, P.chunks[h]));
+                in = !(rhoOk && cluster_culled(pos, dir, rho, dd, P.chunks[h]));
             if (!__ballot(in))
                 continue;
         }
         unsigned cm = 0;
         DSECT_BEGIN(dc3);
-        if (in) {
+        if (in && table) {
+            for (int k = 0; k < nCl; ++k) {
+                const float4 a = W.cl[k][0], b = W.cl[k][1];
+                const ClusterTerms t{V3{a.x, a.y, a.z}, a.w, b.x, b.y};
+                cm |= (unsigned)!(rhoOk && culled_by(t, dir, rho, dd)) << k;
+            }
+        } else if (in) {
             for (int k = 0; k < nCl; ++k)
-                cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, P.clusters[c0 + k])) << k;
+                cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k])) << k;
+        }
+        if (in) {
             /* triangles in the clusters kept (only the scene's last cluster has zero records) */
             tests += (unsigned)__popc(cm) * kClusterSize -
                      (c0 + nCl == P.clusterCount ? ((cm >> (nCl - 1)) & 1u) : 0u) *
@@ -2551,8 +2597,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         int k = 0;       /* samples accumulated */
         unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
         while (k < P.spp && P.maxBounce > 0) {
+            /* window: the state indices the remaining samples likely span (the pixel's hits per sample so far, a
+             * margin; the first window assumes one hit per sample) */
             const int need = P.spp - k;
-            const int nAct = min(64, need + (need >> 4) + 1);
+            const int est = k > 0 ? (int)(((unsigned long long)need * jn + (unsigned)k - 1u) / (unsigned)k) : need;
+            const int nAct = min(64, est + (est >> 3) + 1);
             const bool act = lane < nAct;
             DSECT_BEGIN(dc0);
             /* the lane's start state: the seed advanced by 7 (jn + lane) draws = the wave-uniform state at jn,
@@ -2565,7 +2614,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             int bounce = 0;
             unsigned hits = 0, calls = 0, tests = 0, clTests = 0;
             bool alive = act;
-            for (bool first = true; __any(alive); first = false) {
+            for (int iter = 0; __any(alive); ++iter) {
+                const bool first = iter == 0, bounce1 = iter == 1; /* wave-uniform */
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
                     DSECT_BEGIN(dc1);
@@ -2580,7 +2630,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     DSECT_END(dc1, 1);
                 } else { /* bounce segments of the live lanes (the whole wave takes part) */
                     unsigned t = 0;
-                    c = chain_trace_pairs<MULTI>(P, alive, pos, dir, sRec, W, lane, t);
+                    c = chain_trace_pairs<MULTI>(P, alive, bounce1, pos, dir, sRec, W, lane, t);
                     if (alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
@@ -3350,7 +3400,7 @@ __global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl,
     float excess = 0.f;
     for (int k = 0; k < clusterCount; ++k) {
         const DevCluster K = cl[k];
-        const bool cut = rho <= kClusterRhoMax && cluster_culled(pos, dir, rho, K);
+        const bool cut = rho <= kClusterRhoMax && cluster_culled(pos, dir, rho, dir_dd(dir), K);
         culled += cut;
         for (int j = 0; j < per && k * per + j < recCount; ++j) {
             const DevTri R = clTris[k * per + j];

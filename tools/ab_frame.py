@@ -18,6 +18,8 @@ cfgkw = json.loads(os.environ.get("AB_CFG", "{}"))
 scene_name = cfgkw.pop("scene", "ultracomplex")
 W, H, SPP = cfgkw.pop("W", 1920), cfgkw.pop("H", 1080), cfgkw.pop("spp", 64)
 tris, _ = load_tris(scene_name)
+if cfgkw.pop("empty", False):  # every pixel sky: the sky kernel alone
+    tris = tris[:0]
 ds = rt.DeviceScene(tris, None)
 cfg = rt.RenderConfig(W, H, SPP, 10, True, **cfgkw)
 out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
