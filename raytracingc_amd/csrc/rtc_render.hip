@@ -326,6 +326,33 @@ static DevCluster ball_of(const std::vector<DevTri> &ct, size_t first, size_t co
     return k;
 }
 
+/* A triangle whose stored normal N points along its geometric normal G' = AB x AC closely enough that, for every
+ * ray of |dir|_1 <= kClusterRhoMax, rayTriangle's backface test (dot(dir, N) < 0, raytracing.c:189) forces
+ * det = dot(AB, dir x AC) > -EPSILON (raytracing.c:195): then a hit needs det >= EPSILON, and since
+ * dst = dot(AC, q) / det (q = (pos - A) x AB, raytracing.c:202-206) must be >= EPSILON, dot(AC, q) > 0.  For a
+ * ray origin where the reference's own f32 dot(AC, q) is <= 0 (pos on or behind the plane), the triangle cannot
+ * be hit from there in any direction (rtc_render_chain's first bounces).  Bound: with N = a G'/|G'| + e (e
+ * orthogonal), fl(dot(dir, N)) < 0 gives dir.G'/|G'| < rho (3.01u |N|_inf + |e|) / a, and |det + dir.G'| <=
+ * 5.1u |AB|_1 |AC|_1 rho; aligned when rho times their sum, with a factor 2, stays below EPSILON. */
+static bool aligned_normal(const DevTri &r)
+{
+    const double u = 0x1p-24;
+    const double AB[3] = {r.abx, r.aby, r.abz}, AC[3] = {r.acx, r.acy, r.acz}, N[3] = {r.nx, r.ny, r.nz};
+    const double G[3] = {AB[1] * AC[2] - AB[2] * AC[1], AB[2] * AC[0] - AB[0] * AC[2], AB[0] * AC[1] - AB[1] * AC[0]};
+    const double g = std::sqrt(G[0] * G[0] + G[1] * G[1] + G[2] * G[2]);
+    if (!(g > 0.0) || !std::isfinite(g))
+        return false;
+    const double a = (N[0] * G[0] + N[1] * G[1] + N[2] * G[2]) / g;
+    if (!(a > 0.0))
+        return false;
+    const double e[3] = {N[0] - a * G[0] / g, N[1] - a * G[1] / g, N[2] - a * G[2] / g};
+    const double en = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) + 1e-12 * (std::fabs(N[0]) + std::fabs(N[1]) + std::fabs(N[2]));
+    const double ninf = std::max(std::fabs(N[0]), std::max(std::fabs(N[1]), std::fabs(N[2])));
+    const double n1 = std::fabs(AB[0]) + std::fabs(AB[1]) + std::fabs(AB[2]), c1 = std::fabs(AC[0]) + std::fabs(AC[1]) + std::fabs(AC[2]);
+    const double K = g * (3.01 * u * ninf + en) / a + 5.1 * u * n1 * c1;
+    return std::isfinite(K) && 2.0 * kClusterRhoMax * K < 0.001;
+}
+
 /* ct: the records in cluster order (pad0 = reference index, -1 for padding), cl: one ball per cluster of
  * kClusterSize, ch: one ball per chunk of kChunkClusters consecutive clusters (a subtree of the median split:
  * the chain kernel's first culling level for scenes of more than one chunk) */
@@ -351,6 +378,8 @@ static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std:
             const int i = idx[(size_t)c * kClusterSize + j];
             r = dt[i];
             memcpy(&r.pad0, &i, sizeof i);
+            const int al = aligned_normal(r) ? 1 : 0;
+            memcpy(&r.pad1, &al, sizeof al);
         }
         cl[c] = ball_of(ct, (size_t)c * kClusterSize, kClusterSize);
     }
@@ -2431,6 +2460,43 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records -- or, with
+ * ONE, a (lane, record) pair; the owner's ray from LDS, the exact-safe filter, the reference arithmetic for
+ * survivors, an atomic lexicographic minimum into the owner's key. */
+template <bool MULTI, bool ONE>
+__device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, int c0, const DevTri *__restrict__ sRec,
+                                                  ChainWaveLds &W, int lane)
+{
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        if (i < n) {
+            const unsigned pr = W.pair[i];
+            const int o = (int)(pr & 63u);
+            const float4 rp = W.ray[o][0], rd = W.ray[o][1];
+            const V3 rpos{rp.x, rp.y, rp.z}, rdir{rd.x, rd.y, rd.z};
+            Closest c{999999.f, -1};
+            if (ONE) {
+                const DevTri &R = sRec[pr >> 6];
+                if (general_filter(rpos, rdir, R))
+                    general_exact(rpos, rdir, R, __float_as_int(R.pad0), c);
+            } else {
+                const DevTri *R = (MULTI ? P.clTris : sRec) + (c0 + (int)(pr >> 6)) * kClusterSize;
+                unsigned surv = 0;
+#pragma unroll RTC_CHAIN_UNROLL
+                for (int j = 0; j < kClusterSize; ++j)
+                    surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
+                while (surv) {
+                    const int j = __builtin_ctz(surv);
+                    surv &= surv - 1;
+                    general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
+                }
+            }
+            if (c.idx >= 0 && c.dst < 999999.f)
+                atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
+        }
+    }
+}
+
 template <bool MULTI>
 __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, bool firstBounce, V3 pos,
                                                      V3 dir, const DevTri *__restrict__ sRec, ChainWaveLds &W,
@@ -2442,9 +2508,14 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
     const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
     tests = 0;
-    /* a pixel's first bounces all start at its primary hit point (lane 0's pos): the clusters' origin terms
-     * once, one lane per cluster, into LDS (single-chunk scenes) */
+    /* A pixel's first bounces all start at its primary hit point p0 (lane 0's pos; single-chunk scenes):
+     *  - the clusters' origin terms, once, one lane per cluster, into LDS;
+     *  - the records that can be hit from p0 at all, one lane per record: the reference's own f32
+     *    dot(AC, (p0 - A) x AB) > 0, or a stored normal not aligned with the geometric one (aligned_normal:
+     *    with an aligned normal and that dot <= 0, rayTriangle rejects every direction from p0).
+     * The records that cannot be hit are not tested; the rest are tested as (lane, record) pairs. */
     const bool table = !MULTI && firstBounce;
+    unsigned long long reach[kChunkClusters * kClusterSize / 64];
     if (table) {
         const V3 p0{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.x), 0)),
                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.y), 0)),
@@ -2453,6 +2524,21 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
             const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
             W.cl[lane][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
             W.cl[lane][1] = make_float4(t.A, t.B, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < kChunkClusters * kClusterSize / 64; ++q) {
+            const int i = q * 64 + lane;
+            bool can = false;
+            if (i < P.clusterCount * kClusterSize) {
+                const DevTri &R = sRec[i];
+                if (__float_as_int(R.pad0) >= 0) {
+                    const V3 sv = sub(p0, V3{R.ax, R.ay, R.az});               /* raytracing.c:198 */
+                    const V3 qv = cross(sv, V3{R.abx, R.aby, R.abz});          /* :202 */
+                    const float dac = dot(V3{R.acx, R.acy, R.acz}, qv);        /* :206 numerator */
+                    can = dac > 0.f || __float_as_int(R.pad1) == 0;
+                }
+            }
+            reach[q] = __ballot(can);
         }
         wave_lds_sync();
     }
@@ -2472,15 +2558,19 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_BEGIN(dc3);
         if (in && table) {
             for (int k = 0; k < nCl; ++k) {
+                const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
+                if (!r8)
+                    continue; /* no record of the cluster can be hit from p0 */
                 const float4 a = W.cl[k][0], b = W.cl[k][1];
                 const ClusterTerms t{V3{a.x, a.y, a.z}, a.w, b.x, b.y};
-                cm |= (unsigned)!(rhoOk && culled_by(t, dir, rho, dd)) << k;
+                if (!(rhoOk && culled_by(t, dir, rho, dd))) {
+                    cm |= 1u << k;
+                    tests += (unsigned)__popc(r8);
+                }
             }
         } else if (in) {
             for (int k = 0; k < nCl; ++k)
                 cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k])) << k;
-        }
-        if (in) {
             /* triangles in the clusters kept (only the scene's last cluster has zero records) */
             tests += (unsigned)__popc(cm) * kClusterSize -
                      (c0 + nCl == P.clusterCount ? ((cm >> (nCl - 1)) & 1u) : 0u) *
@@ -2489,41 +2579,47 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
         int n = 0;
-        for (int k = 0; k < nCl; ++k) {
-            const unsigned long long m = __ballot((cm >> k) & 1u);
-            if ((cm >> k) & 1u)
-                W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
-                    (unsigned short)(lane | (k << 6));
-            n += (int)__popcll(m);
+        if (table) {
+            /* (lane, record) entries for the reachable records of the clusters each lane kept; the list is
+             * flushed through the passes whenever the next cluster would overflow it */
+            constexpr int kCap = (int)(sizeof(W.pair) / sizeof(W.pair[0]));
+            for (int k = 0; k < nCl; ++k) {
+                const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
+                const unsigned long long m = __ballot((cm >> k) & 1u);
+                if (!m)
+                    continue;
+                const int per = __popc(r8), cnt = (int)__popcll(m) * per;
+                if (n + cnt > kCap) {
+                    wave_lds_sync();
+                    chain_pair_passes<MULTI, true>(P, n, c0, sRec, W, lane);
+                    wave_lds_sync();
+                    n = 0;
+                }
+                if ((cm >> k) & 1u) {
+                    int e = n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) * per;
+                    for (unsigned r = r8; r; r &= r - 1)
+                        W.pair[e++] = (unsigned short)(lane | ((k * kClusterSize + __builtin_ctz(r)) << 6));
+                }
+                n += cnt;
+            }
+        } else {
+            for (int k = 0; k < nCl; ++k) {
+                const unsigned long long m = __ballot((cm >> k) & 1u);
+                if ((cm >> k) & 1u)
+                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                        (unsigned short)(lane | (k << 6));
+                n += (int)__popcll(m);
+            }
         }
         wave_lds_sync();
         DSECT_END(dc4, 4);
         DSECT_BEGIN(dc5);
-        for (int b = 0; b < n; b += 64) {
-            const int i = b + lane;
-            if (i < n) {
-                const unsigned pr = W.pair[i];
-                const int o = (int)(pr & 63u), k = c0 + (int)(pr >> 6);
-                const float4 rp = W.ray[o][0], rd = W.ray[o][1];
-                const V3 rpos{rp.x, rp.y, rp.z}, rdir{rd.x, rd.y, rd.z};
-                const DevTri *R = (MULTI ? P.clTris : sRec) + k * kClusterSize;
-                unsigned surv = 0;
-#pragma unroll RTC_CHAIN_UNROLL
-                for (int j = 0; j < kClusterSize; ++j)
-                    surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
-                if (surv) {
-                    Closest c{999999.f, -1};
-                    while (surv) {
-                        const int j = __builtin_ctz(surv);
-                        surv &= surv - 1;
-                        general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
-                    }
-                    if (c.idx >= 0 && c.dst < 999999.f)
-                        atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
-                }
-            }
-        }
+        if (table)
+            chain_pair_passes<MULTI, true>(P, n, c0, sRec, W, lane);
+        else
+            chain_pair_passes<MULTI, false>(P, n, c0, sRec, W, lane);
         wave_lds_sync(); /* the pair list is rewritten by the next chunk */
         DSECT_END(dc5, 5);
     }

@@ -177,7 +177,9 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
         tests.append(s3["tri_tests"])
     assert tests[0] == tests[1]
     if sph is None or len(sph) == 0:
-        assert s1["tri_tests"] == tests[0] and s4["tri_tests"] == tests[0]
+        # the state-indexed kernel also skips, for first bounces, the records that cannot be hit from the
+        # pixel's primary hit point (aligned_normal): fewer or equal tests
+        assert s1["tri_tests"] <= tests[0] and s4["tri_tests"] == tests[0]
     # the state-indexed kernel summing each pixel's samples itself (RTC_F_CHAIN_INLINE) == the deferred pass
     c6, a6, s6 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "chain_inline": True}),
                            want_accum=True)
