@@ -187,9 +187,10 @@ int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *unif
  * per-triangle test it must never contradict): clusters `tris` as rtc_scene_upload does and, for every ray and
  * every cluster ball (8 triangles) and chunk ball (32 clusters, scenes of more than one chunk), counts [0] hits
  * inside balls the ray was culled from (0 when sound), [1] balls culled, [2] ball tests, [3] hits, [4] float
- * bits of the largest hit-point excess over a ball's radius. */
+ * bits of the largest hit-point excess over a ball's radius, [5] hits on triangles the first-bounce reach mask
+ * calls unreachable from the ray's origin (0 when sound), [6] (ray, triangle) pairs it calls so. */
 int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
-                            unsigned long long counts[5]);
+                            unsigned long long counts[7]);
 
 #ifdef __cplusplus
 }

@@ -321,10 +321,12 @@ def random_sequences(seeds: np.ndarray, draws: int):
 
 def cluster_bound_probe(tris: np.ndarray, rays: np.ndarray) -> dict:
     """Soundness of the bounce-ray cluster culling on the GPU (rtc_probe_cluster_bound): hits inside culled
-    clusters (must be 0), clusters culled, cluster tests, hits, largest hit excess over a bounding radius."""
+    clusters (must be 0), clusters culled, cluster tests, hits, largest hit excess over a bounding radius; hits
+    on triangles the first-bounce reach mask calls unreachable from the ray's origin (must be 0), pairs so called."""
     t = np.ascontiguousarray(tris, TRIANGLE_DT)
     r = np.ascontiguousarray(rays, RAY_DT)
-    c = np.zeros(5, np.uint64)
+    c = np.zeros(7, np.uint64)
     check(lib().rtc_probe_cluster_bound(_ptr(t), len(t), _ptr(r), len(r), _ptr(c)), "rtc_probe_cluster_bound")
     return {"violations": int(c[0]), "culled": int(c[1]), "tests": int(c[2]), "hits": int(c[3]),
-            "max_excess": float(np.array([c[4]], np.uint64).astype(np.uint32).view(np.float32)[0])}
+            "max_excess": float(np.array([c[4]], np.uint64).astype(np.uint32).view(np.float32)[0]),
+            "reach_violations": int(c[5]), "unreachable": int(c[6])}

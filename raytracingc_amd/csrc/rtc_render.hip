@@ -2513,8 +2513,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
      *  - the records that can be hit from p0 at all, one lane per record: the reference's own f32
      *    dot(AC, (p0 - A) x AB) > 0, or a stored normal not aligned with the geometric one (aligned_normal:
      *    with an aligned normal and that dot <= 0, rayTriangle rejects every direction from p0).
-     * The records that cannot be hit are not tested; the rest are tested as (lane, record) pairs. */
-    const bool table = !MULTI && firstBounce;
+     * The records that cannot be hit are not tested; the rest are tested as (lane, record) pairs.  The argument
+     * holds for |dir|_1 <= kClusterRhoMax: a wave with a live ray beyond that takes the per-cluster path. */
+    const bool table = !MULTI && firstBounce && P.clusterCull && !__ballot(alive && !rhoOk);
     unsigned long long reach[kChunkClusters * kClusterSize / 64];
     if (table) {
         const V3 p0{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.x), 0)),
@@ -3483,16 +3484,19 @@ __global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, 
 /* Cluster culling soundness (DevCluster): every (ray, cluster) pair is culled or not by cluster_culled, and
  * every triangle of the cluster is tested with the reference's rayTriangle arithmetic.  counts: [0] hits in
  * culled clusters (must stay 0), [1] clusters culled, [2] cluster tests, [3] hits, [4] float bits of the
- * largest (distance from the ball centre to the reported hit point) - r over all hits. */
+ * largest (distance from the ball centre to the reported hit point) - r over all hits; with reach, [5] hits on
+ * records judged unreachable from the ray's origin (aligned_normal; must stay 0), [6] (ray, record) pairs judged
+ * so. */
 __global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl, int clusterCount, int per,
-                                     int recCount, const Ray *rays, size_t n, unsigned long long *counts)
+                                     int recCount, bool reach, const Ray *rays, size_t n,
+                                     unsigned long long *counts)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     const V3 pos = v3(rays[i].pos), dir = v3(rays[i].dir);
     const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
-    unsigned viol = 0, culled = 0, hits = 0;
+    unsigned viol = 0, culled = 0, hits = 0, unreachHits = 0, unreach = 0;
     float excess = 0.f;
     for (int k = 0; k < clusterCount; ++k) {
         const DevCluster K = cl[k];
@@ -3502,11 +3506,17 @@ __global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl,
             const DevTri R = clTris[k * per + j];
             if (__float_as_int(R.pad0) < 0)
                 continue;
+            /* rtc_render_chain's first-bounce reach mask: not hittable from pos in any direction */
+            const V3 q = cross(sub(pos, V3{R.ax, R.ay, R.az}), V3{R.abx, R.aby, R.abz});
+            const bool cannot = reach && rho <= kClusterRhoMax && __float_as_int(R.pad1) != 0 &&
+                                !(dot(V3{R.acx, R.acy, R.acz}, q) > 0.f);
+            unreach += cannot;
             float dst;
             if (ray_triangle(pos, dir, V3{R.ax, R.ay, R.az}, V3{R.abx, R.aby, R.abz}, V3{R.acx, R.acy, R.acz},
                              V3{R.nx, R.ny, R.nz}, dst)) {
                 hits++;
                 viol += cut;
+                unreachHits += cannot;
                 const V3 h = add(pos, mul(dir, dst));
                 const V3 w = sub(h, V3{K.cx, K.cy, K.cz});
                 excess = fmaxf(excess, (float)__builtin_sqrt((double)dot(w, w)) - K.r);
@@ -3518,6 +3528,10 @@ __global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl,
     atomicAdd(&counts[2], (unsigned long long)clusterCount);
     atomicAdd(&counts[3], (unsigned long long)hits);
     atomicMax(&counts[4], (unsigned long long)__float_as_uint(excess));
+    if (reach) {
+        atomicAdd(&counts[5], (unsigned long long)unreachHits);
+        atomicAdd(&counts[6], (unsigned long long)unreach);
+    }
 }
 
 namespace {
@@ -3642,11 +3656,11 @@ extern "C" int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, 
 }
 
 extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
-                                       unsigned long long counts[5])
+                                       unsigned long long counts[7])
 {
     if (!counts || triCount < 0 || (triCount > 0 && !tris) || (n > 0 && !rays))
         return rtc_fail(RTC_EINVAL, "rtc_probe_cluster_bound: bad argument");
-    memset(counts, 0, 5 * sizeof(unsigned long long));
+    memset(counts, 0, 7 * sizeof(unsigned long long));
     if (int rc = probe_prelude())
         return rc;
     if (n == 0 || triCount == 0)
@@ -3662,22 +3676,23 @@ extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const
     if (e == hipSuccess)
         e = hipMemcpy(dr, rays, n * sizeof(Ray), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = sc.alloc((void **)&dc, 5 * sizeof(unsigned long long));
+        e = sc.alloc((void **)&dc, 7 * sizeof(unsigned long long));
     if (e == hipSuccess)
-        e = hipMemset(dc, 0, 5 * sizeof(unsigned long long));
+        e = hipMemset(dc, 0, 7 * sizeof(unsigned long long));
     if (e == hipSuccess) {
         /* the clusters, then the chunks (balls over kChunkClusters clusters, rtc_render_chain's first level) */
         hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->clusters,
-                           s->clusterCount, kClusterSize, s->clusterCount * kClusterSize, dr, n, dc);
+                           s->clusterCount, kClusterSize, s->clusterCount * kClusterSize, true, dr, n, dc);
         e = hipGetLastError();
         if (e == hipSuccess && s->chunkCount > 1) {
             hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->chunks,
-                               s->chunkCount, kClusterSize * kChunkClusters, s->clusterCount * kClusterSize, dr, n, dc);
+                               s->chunkCount, kClusterSize * kChunkClusters, s->clusterCount * kClusterSize, false, dr, n,
+                               dc);
             e = hipGetLastError();
         }
     }
     if (e == hipSuccess)
-        e = hipMemcpy(counts, dc, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+        e = hipMemcpy(counts, dc, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     if (e != hipSuccess)
         rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
     rtc_scene_release(s);

@@ -75,6 +75,20 @@ def _grazing_rays(tris, n, rng):
     return pos, d
 
 
+def _self_rays(tris, n, rng):
+    """Origins on (or a hair off) a triangle's plane, aimed along that plane and slightly through it: the
+    reference's dot(AC, (pos - A) x AB) near 0, where the first-bounce reach mask decides."""
+    A, B, C, N = _verts(tris)
+    k = rng.integers(0, len(tris), n)
+    w = rng.dirichlet([1, 1, 1], n) * 1.4 - 0.2  # inside and just outside the triangle
+    pos = w[:, :1] * A[k] + w[:, 1:2] * B[k] + w[:, 2:] * C[k]
+    pos += N[k] * (rng.normal(size=(n, 1)) * 10.0 ** rng.uniform(-8, -3, (n, 1)))
+    w2 = rng.dirichlet([1, 1, 1], n)
+    d = _unit(w2[:, :1] * A[k] + w2[:, 1:2] * B[k] + w2[:, 2:] * C[k] - pos + 1e-30)
+    d = d - N[k] * np.sum(d * N[k], 1, keepdims=True)
+    return pos, _unit(d + 1e-30) - N[k] * (rng.choice([-1.0, 1.0], (n, 1)) * 10.0 ** rng.uniform(-7, 0, (n, 1)))
+
+
 def _free_rays(tris, n, rng):
     A, B, C, _ = _verts(tris)
     lo = np.minimum(np.minimum(A, B), C).min(0)
@@ -85,8 +99,9 @@ def _free_rays(tris, n, rng):
 
 
 def _rays(tris, n, rng):
-    parts = [g(tris, n, rng) for g in (_bounce_like_rays, _aimed_rays, _grazing_rays, _free_rays)]
-    r = np.zeros(4 * n, RAY_DT)
+    gens = (_bounce_like_rays, _aimed_rays, _grazing_rays, _self_rays, _free_rays)
+    parts = [g(tris, n, rng) for g in gens]
+    r = np.zeros(len(gens) * n, RAY_DT)
     pos = np.concatenate([p for p, _ in parts]).astype(np.float32)
     d = np.concatenate([d for _, d in parts]).astype(np.float32)
     for i, c in enumerate("xyz"):
@@ -115,6 +130,9 @@ def test_cluster_culling_is_sound(name, scale, gpu_available):
     r = rt.cluster_bound_probe(tris, rays)
     print(name, scale, r)
     assert r["violations"] == 0, r
+    assert r["reach_violations"] == 0, r
     assert r["hits"] > 1_000
+    if scale <= 1.0:  # aligned_normal's margin is absolute (EPSILON): large triangles are never "aligned"
+        assert r["unreachable"] > 0
     if len(tris) > 16 and scale == 1.0:
         assert r["culled"] > r["tests"] // 8  # the bound is not vacuous
