@@ -369,7 +369,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic,
-                         "kernel": "rtc_render_heavy (heavy-tile kernel of the split launch)",
+                         "kernel": "rtc_render_chain (geometry pixels of the split launch; state-indexed samples)",
                          "kernel_ms": round(dom_ms, 4),
                          "sky_kernel_ms": round(sky_ms, 4) if sky_ms else None,
                          "work_per_launch": f"{tests_per_launch:.4g} ray-triangle tests x {FLOPS_PER_TEST} flop",

@@ -138,6 +138,9 @@ __device__ __forceinline__ float rng_value_of_state(unsigned s)
 __device__ __forceinline__ float random_normal(unsigned &s)
 {
     float theta = (float)(2 * 3.14159265 * (double)random_value(s));
+#ifdef RTC_FAKE_BM /* timing experiment only: not the reference's value */
+    return __fsqrt_rn(-2.f * __logf(random_value(s))) * __cosf(theta);
+#endif
     float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)random_value(s)));
     return (float)((double)rho * rtcmath::cos((double)theta));
 }
@@ -156,6 +159,7 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
 struct EnvParams {
     V3 sun, horizon, zenith, ground;
     float focus, intensity;
+    bool sunSkip; /* env_sun_skippable(focus, intensity) */
     /* powf tables (null: glibc's constants in global memory; kernels point them at LDS copies) */
     const double (*log2tab)[2];
     const unsigned long long *exp2tab;
@@ -189,14 +193,42 @@ struct PowTablesLds {
 };
 
 /* getEnvironmentLight (raytracing.c:151-160) */
+/* fmax(0, v) as the reference's libm evaluates it (raytracing.c:155, double fmax of a float): NaN -> 0, v < 0
+ * -> +0, otherwise v itself -- -0 included (x86-64 glibc returns its second operand for equal zeros) */
+__device__ __forceinline__ float fmax0_ref(float v) { return (v < 0.f || v != v) ? 0.f : v; }
+/* fmax(x, y) likewise (raytracing.c:283, Russian roulette): x > y ? x : y, the other operand when one is NaN;
+ * y for equal values (the sign of equal zeros) */
+__device__ __forceinline__ float fmax_ref(float x, float y) { return (x > y || y != y) ? x : y; }
+
+/* Whether getEnvironmentLight's sun term sun * sunMask (raytracing.c:155-158) is known without its powf when
+ * x = fmax(0, dot(dir, sunDir)) is +0 or the mask is 0 with x <= 1 (x not -0): with focus > 0, powf(x, focus)
+ * is then a finite value >= +0 (+0 for x = +0, <= 1 for x <= 1), and with a finite intensity the product is a
+ * zero of intensity's sign. */
+__host__ __device__ __forceinline__ bool env_sun_skippable(float focus, float intensity)
+{
+    return focus > 0.f && intensity - intensity == 0.f; /* focus > 0, intensity finite */
+}
+
+/* getEnvironmentLight (raytracing.c:151-160).  A powf whose value is known for every live lane of the wave is
+ * not evaluated (a wave-uniform branch, values unchanged): skyGradientT when smoothstep gives +0 (powf(+0, .35)
+ * = +0) -- rays below the horizon --, the sun term as env_sun_skippable says. */
 __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
 {
-    float skyGradientT = pow_ref(smoothstep(0.f, 0.74f, -dir.y), 0.35f, s);
+    const float skyArg = smoothstep(0.f, 0.74f, -dir.y);
+    float skyGradientT = 0.f;
+    if (__any(__float_as_uint(skyArg) != 0u))
+        skyGradientT = pow_ref(skyArg, 0.35f, s);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
-    float sun = pow_ref(fmaxf(0.f, dot(dir, s.sun)), s.focus, s) * s.intensity;
+    const float sunArg = fmax0_ref(dot(dir, s.sun));
     float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
     float sunMask = dir.y < 0.f ? 1.f : 0.f;
-    float sv = sun * sunMask;
+    float sv = __builtin_copysignf(0.f, s.intensity);
+    const bool sunKnown = s.sunSkip && __float_as_uint(sunArg) != 0x80000000u && /* powf(-0, odd) = -0 */
+                          (sunArg == 0.f || (sunMask == 0.f && sunArg <= 1.f));
+    if (__any(!sunKnown)) {
+        const float sun = pow_ref(sunArg, s.focus, s) * s.intensity;
+        sv = sun * sunMask;
+    }
     return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
 }
 

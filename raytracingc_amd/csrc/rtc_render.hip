@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
                 const V3 emitted = mul(color, emission);
                 light = add(light, mulv(emitted, rayColor));
                 rayColor = mulv(rayColor, color);
-                const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
                 endSample = p < random_value(rng);
                 if (!endSample) {
                     rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
@@ -1810,7 +1810,7 @@ template <int KC>
 __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub)
 {
     const float sky = smoothstep(0.f, 0.74f, -dir.y);
-    const float sunDot = fmaxf(0.f, dot(dir, s.sun));
+    const float sunDot = fmax0_ref(dot(dir, s.sun));
     const bool second = (sub & 1) != 0;
     const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f, s);
     const float skyGradientT = group_lane<KC, 0>(pw, sub);
@@ -2038,7 +2038,7 @@ __global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEA
                     const V3 emitted = mul(color, M.emission);
                     light = add(light, mulv(emitted, rayColor));
                     rayColor = mulv(rayColor, color);
-                    const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                    const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
                     endSample = p < random_value(rng);
                     if (!endSample) {
                         rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
@@ -2341,7 +2341,7 @@ __global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
                         const V3 emitted = mul(color, M.emission);
                         light = add(light, mulv(emitted, rayColor));
                         rayColor = mulv(rayColor, color);
-                        const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                        const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
                         endSample = p < random_value(rng);
                         draws += 7;
                         if (!endSample) {
@@ -2444,14 +2444,21 @@ constexpr int kChainWorkers = 2048;
  * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
 typedef float f2 __attribute__((ext_vector_type(2)));
+#ifndef RTC_CHAIN_PAIRS
+#define RTC_CHAIN_PAIRS 1024
+#endif
 struct ChainWaveLds {
     float4 ray[64][2];            /* pos, dir of each lane's segment */
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
-    unsigned short pair[64 * 32]; /* lane | cluster << 6, cluster-major */
+    /* lane | cluster << 6 (or lane | record << 6), cluster-major; a full list is run through the passes and
+     * refilled.  Its size keeps a block (4 waves + the staged records of one chunk) within 40 KB of LDS: four
+     * blocks per CU, the 4 waves per SIMD that 128 VGPRs allow */
+    unsigned short pair[RTC_CHAIN_PAIRS];
 };
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
-static_assert(kChunkClusters <= 32, "the pair list holds one chunk of clusters per lane");
+static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
+static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -2580,10 +2587,10 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
         int n = 0;
+        constexpr int kCap = RTC_CHAIN_PAIRS;
         if (table) {
             /* (lane, record) entries for the reachable records of the clusters each lane kept; the list is
              * flushed through the passes whenever the next cluster would overflow it */
-            constexpr int kCap = (int)(sizeof(W.pair) / sizeof(W.pair[0]));
             for (int k = 0; k < nCl; ++k) {
                 const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
                 const unsigned long long m = __ballot((cm >> k) & 1u);
@@ -2607,6 +2614,14 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         } else {
             for (int k = 0; k < nCl; ++k) {
                 const unsigned long long m = __ballot((cm >> k) & 1u);
+                if (!m)
+                    continue;
+                if (n + (int)__popcll(m) > kCap) {
+                    wave_lds_sync();
+                    chain_pair_passes<MULTI, false>(P, n, c0, sRec, W, lane);
+                    wave_lds_sync();
+                    n = 0;
+                }
                 if ((cm >> k) & 1u)
                     W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
@@ -2751,7 +2766,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         const V3 emitted = mul(color, M.emission);
                         light = add(light, mulv(emitted, rayColor));
                         rayColor = mulv(rayColor, color);
-                        const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                        const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
                         endSample = p < random_value(rng);
                         if (!endSample) {
                             rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
@@ -3051,7 +3066,7 @@ __global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
                     const V3 emitted = mul(color, M.emission);
                     light = add(light, mulv(emitted, rayColor));
                     rayColor = mulv(rayColor, color);
-                    const float p = fmaxf(fmaxf(rayColor.x, rayColor.y), rayColor.z);
+                    const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
                     endSample = p < random_value(rng);
                     draws += 7;
                     if (!endSample) {
@@ -3158,6 +3173,7 @@ static EnvParams env_of(const Scene &s)
     e.ground = V3{s.groundColor.x, s.groundColor.y, s.groundColor.z};
     e.focus = s.sunFocus;
     e.intensity = s.sunIntensity;
+    e.sunSkip = env_sun_skippable(e.focus, e.intensity);
     return e;
 }
 
@@ -3346,8 +3362,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                        (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
                 else
                     hipLaunchKernelGGL(rtc_render_chain<true>, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
+                HIP_TRY(hipGetLastError());
+                if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
+                    HIP_TRY(hipEventRecord(s->evHeavy1, st));
                 if (P.sampleCap > 0) {
-                    HIP_TRY(hipGetLastError());
                     const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
                     hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
                 }
@@ -3361,7 +3379,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             else
                 hipLaunchKernelGGL(rtc_render_heavy<4>, workers, dim3(64 * 4), rtc_heavy_lds_bytes(s->triPadded), st, P);
             HIP_TRY(hipGetLastError());
-            if (s->timing)
+            if (s->timing && !chain)
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
             ms->timed = s->timing;
             if (RTC_SIDE_STREAM)
@@ -3459,6 +3477,7 @@ __global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n,
     e.ground = v3(s.groundColor);
     e.focus = s.sunFocus;
     e.intensity = s.sunIntensity;
+    e.sunSkip = env_sun_skippable(e.focus, e.intensity);
     V3 c = environment(v3(rays[i].dir), e);
     out[i] = vec3{c.x, c.y, c.z};
 }

@@ -11,6 +11,7 @@ the deterministic variant described in SURVEY.md F4 (oracle/ref_unity.c, oracle/
   kat_tri.npz            rayTriangle on random + constructed edge-case (ray, triangle) pairs
   kat_sphere.npz         raySphere
   kat_env.npz            getEnvironmentLight
+  kat_env_edge.npz       getEnvironmentLight at signed zeros, special sun intensities / focus values
   kat_calc_<scene>.npz   calcColor per (ray, seed, maxBounce)
   kat_debug_<scene>.npz  calcDebugColor (raytracing.c:242-260) per (ray, seed, maxBounce)
   render_golden.json     full renders (main.c render loop): sha256 of the pre-quantisation float
@@ -401,9 +402,59 @@ def gen_meta():
         json.dump(meta, f, indent=1, sort_keys=True)
 
 
+def gen_kat_env_edge(work):
+    """getEnvironmentLight at the values where a powf's result is known without evaluating it (the device
+    skips those powf calls wave by wave): rays below the horizon, the sun behind the ray, signed zeros, a
+    negative / zero / infinite / NaN sun intensity, sun focus 0, odd integers, fractions and negatives."""
+    rng = np.random.default_rng(20261016)
+    n = 4096
+    d = rand_unit(rng, n)
+    d[:512, 1] = np.abs(d[:512, 1])  # below the horizon (+y is down after the loader's flip)
+    d[512:1024, 1] = -np.abs(d[512:1024, 1])
+    zeros = np.array([[0, 0, 0], [-0.0, -0.0, -0.0], [0, -0.0, 0], [-0.0, 0, -0.0], [0, 0, 1], [0, -0.0, 1],
+                      [0, 0, -1], [1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, -0.0, -1]], np.float32)
+    d[1024:1024 + len(zeros)] = zeros
+    d[1100:1200] = np.nan
+    rays = np.zeros(n, RAY_DT)
+    for k, f in enumerate("xyz"):
+        rays["dir"][f] = d[:, k]
+    scenes = np.zeros(n, SCENE_DT)
+
+    def setv(name, v):
+        for k, f in enumerate("xyz"):
+            scenes[name][f] = v[:, k]
+
+    sun = rand_unit(rng, n)
+    sun[::7] = d[::7]  # the sun along the ray, and opposite it
+    sun[3::7] = -d[3::7]
+    sun[5::11] = np.array([0, 0, 0], np.float32)
+    sun = np.where(np.isnan(sun), np.float32(0), sun)
+    setv("normalizedSunDirection", sun)
+    setv("skyColorHorizon", rng.random((n, 3)).astype(np.float32))
+    setv("skyColorZenith", rng.random((n, 3)).astype(np.float32))
+    g = rng.random((n, 3)).astype(np.float32)
+    g[::13] = np.float32(-0.0)
+    g[1::13] = np.float32(0.0)
+    setv("groundColor", g)
+    scenes["sunFocus"] = rng.choice(np.array([0, 1, 2, 3, 5, 7.5, 22, 100, -1, -3, 0.5, 1e-30], np.float32), n)
+    scenes["sunIntensity"] = rng.choice(np.array([0.75, -0.75, 0, -0.0, np.inf, -np.inf, np.nan, 3, 1e30],
+                                                 np.float32), n)
+    kin = np.zeros(n, np.dtype([("ray", RAY_DT), ("s", SCENE_DT)]))
+    kin["ray"], kin["s"] = rays, scenes
+    fi, fo = os.path.join(work, "env_edge.in"), os.path.join(work, "env_edge.out")
+    kin.tofile(fi)
+    run_ref(["--kat-env", fi, fo], work)
+    out = np.fromfile(fo, np.float32).reshape(n, 3)
+    np.savez_compressed(os.path.join(HERE, "kat_env_edge.npz"), rays=rays, scenes=scenes, out=out)
+
+
 def main():
     if not os.path.exists(REF_BIN):
         sys.exit(f"{REF_BIN} missing: run `make ref` (needs {REF_DIR})")
+    if sys.argv[1:] == ["--env-edge"]:  # the one fixture added later (its own seed; the others unchanged)
+        with tempfile.TemporaryDirectory() as work:
+            gen_kat_env_edge(work)
+        return
     rng = np.random.default_rng(20251003)
     with tempfile.TemporaryDirectory() as work:
         # default mode reads ./triangles.txt (main.c:237): give the reference a private working dir
@@ -418,6 +469,7 @@ def main():
         for s in ["ultracomplex", "default"]:
             gen_kat_calc(work, rng, s, debug=True)
         gen_renders(work)
+        gen_kat_env_edge(work)
         gen_meta()
 
 

@@ -49,8 +49,9 @@ def test_ray_sphere_kat():
     assert np.array_equal(_bits(nrm[m]), _bits(k["normal"][m]))
 
 
-def test_environment_kat():
-    k = np.load(f"{GOLDEN}/kat_env.npz")
+@pytest.mark.parametrize("fixture", ["kat_env", "kat_env_edge"])
+def test_environment_kat(fixture):
+    k = np.load(f"{GOLDEN}/{fixture}.npz")
     out = orc.environment(k["rays"], k["scenes"])
     assert np.array_equal(_bits(out), _bits(k["out"]))
 

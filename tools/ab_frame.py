@@ -51,7 +51,10 @@ while args and args[0].startswith("--"):
         args = args[2:]
     elif args[0] == "--cfg":
         k, v = args[1].split("=", 1)
-        cfg[k] = json.loads(v)
+        try:
+            cfg[k] = json.loads(v)
+        except json.JSONDecodeError:
+            cfg[k] = v  # a bare string (scene=fsuzane)
         args = args[2:]
 for lib in args:
     env = dict(os.environ, REPO=REPO, AB_FRAMES=frames, AB_CFG=json.dumps(cfg),
