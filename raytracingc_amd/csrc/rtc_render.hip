@@ -2676,6 +2676,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * (l: the sub-list of item `it`, base: its first item, cnt: its length) */
     const int tilesX = P.blocksX * 2;
     unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segSpec = 0, segClusters = 0;
+#ifdef RTC_DIAG
+    unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
+#endif
     int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
     for (int it = gw;; it += nWaves) {
         while (it - base >= cnt && l < kGeoLists - 1) {
@@ -2728,6 +2731,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             bool alive = act;
             for (int iter = 0; __any(alive); ++iter) {
                 const bool first = iter == 0, bounce1 = iter == 1; /* wave-uniform */
+#ifdef RTC_DIAG
+                dIters++;
+                dAlive += (unsigned long long)__popcll(__ballot(alive));
+#endif
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
                     DSECT_BEGIN(dc1);
@@ -2860,6 +2867,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 wave_lds_sync(); /* the ray slots are rewritten by the next round */
             }
             jn += (unsigned)p;
+#ifdef RTC_DIAG
+            dWindows++;
+            dAct += (unsigned)nAct;
+            dUsed += (unsigned long long)__popcll(__ballot(mult > 0));
+#endif
             /* counters: committed samples (with multiplicity) and the tests of the discarded ones */
             segCalls += (unsigned long long)mult * calls;
             segTraced += (unsigned long long)mult * (P.hoist ? calls - 1u : calls);
@@ -2887,6 +2899,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #ifdef RTC_DIAG
     if (lane < 8)
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
+    /* [8] bounce-loop iterations, [9] live lanes summed over them, [10] window lanes, [11] windows, [12] lanes
+     * whose sample was used */
+    if (lane == 0) {
+        atomicAdd(&g_rtc_sect[8], dIters);
+        atomicAdd(&g_rtc_sect[9], dAlive);
+        atomicAdd(&g_rtc_sect[10], dAct);
+        atomicAdd(&g_rtc_sect[11], dWindows);
+        atomicAdd(&g_rtc_sect[12], dUsed);
+    }
 #endif
     flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
 }

@@ -25,6 +25,10 @@ for hoist in (False, True):
     _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
     L.rtc_diag_sections(out, 1)
     tot = sum(out[i] for i in range(8))
+    it, alive, act, win, used = (out[i] for i in range(8, 13))
+    print(json.dumps({"hoist": hoist, "iterations": it, "lane_utilisation": round(alive / max(1, 64 * it), 4),
+                      "window_lanes_per_window": round(act / max(1, win), 2), "used_lanes_share": round(used / max(1, act), 4),
+                      "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
     print(json.dumps({"hoist": hoist, "render_ms": round(st["render_ms"], 3),
                       "share": {n: round(out[i] / tot, 4) for i, n in enumerate(names)},
                       "cycles": {n: int(out[i]) for i, n in enumerate(names)}}), flush=True)
