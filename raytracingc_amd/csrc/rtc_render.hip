@@ -1823,12 +1823,21 @@ __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int s
     return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
 }
 
+/* LDS writes of this wave visible to its other lanes (the wave is the only user of the region) */
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 /* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile of a 16x16 block; the waves of
  * tiles with primary candidates return at once (rtc_render_heavy renders those).  Few registers, so many
  * waves per SIMD hide the latency of the environment's double-precision chains. */
 __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const unsigned *__restrict__ tileW)
 {
     __shared__ PowTablesLds sPow;
+    __shared__ __attribute__((aligned(4))) unsigned char sSkyRow[kBlock / 64][8][24];
     sPow.fill(threadIdx.x);
     __syncthreads();
     sPow.attach(P.env);
@@ -1862,11 +1871,38 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
             segCalls = (unsigned)P.spp;
             segTraced = P.hoist ? 1u : (unsigned)P.spp;
         }
+        /* Color[] (vec3ToColor, main.c:101): a tile row whose 8 pixels are all this kernel's goes out as six
+         * dword stores of its 24 bytes (staged in LDS) instead of 24 byte stores; rows shared with geometry
+         * pixels (written by the other kernel) or cut by the frame edge keep byte stores */
+        const unsigned char c0 = float_to_u8(acc.x), c1 = float_to_u8(acc.y), c2 = float_to_u8(acc.z);
+        const unsigned long long full = __ballot(px.valid);
+        const int row = lane >> 3;
+        const bool aligned = (P.width & 3) == 0 && ((size_t)P.colors & 3) == 0;
+        const bool packed = aligned && ((full >> (row * 8)) & 0xffull) == 0xffull;
+        unsigned char *rowBytes = sSkyRow[threadIdx.x >> 6][row];
+        if (packed) {
+            rowBytes[3 * (lane & 7)] = c0;
+            rowBytes[3 * (lane & 7) + 1] = c1;
+            rowBytes[3 * (lane & 7) + 2] = c2;
+        }
+        wave_lds_sync();
+        if (lane < 48) {
+            const int rr = lane / 6, dw = lane - rr * 6;
+            if (aligned && ((full >> (rr * 8)) & 0xffull) == 0xffull) {
+                /* this row's first pixel: column 0 of the tile, row rr */
+                const int x0 = blockIdx.x * kTileW + ((threadIdx.x >> 6) & 1) * 8;
+                const int r0 = blockIdx.y * kTileH + ((threadIdx.x >> 6) >> 1) * 8 + rr;
+                unsigned *dst = (unsigned *)(P.colors + 3 * ((size_t)r0 * (size_t)P.width + (size_t)x0));
+                dst[dw] = ((const unsigned *)sSkyRow[threadIdx.x >> 6][rr])[dw];
+            }
+        }
         if (px.valid) {
             const size_t o = (size_t)px.r * (size_t)P.width + (size_t)px.x;
-            P.colors[3 * o] = float_to_u8(acc.x);
-            P.colors[3 * o + 1] = float_to_u8(acc.y);
-            P.colors[3 * o + 2] = float_to_u8(acc.z);
+            if (!packed) {
+                P.colors[3 * o] = c0;
+                P.colors[3 * o + 1] = c1;
+                P.colors[3 * o + 2] = c2;
+            }
             if (P.accum) {
                 P.accum[3 * o] = acc.x;
                 P.accum[3 * o + 1] = acc.y;
@@ -2459,13 +2495,6 @@ struct ChainWaveLds {
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
 static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
-
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records -- or, with
  * ONE, a (lane, record) pair; the owner's ray from LDS, the exact-safe filter, the reference arithmetic for
