@@ -1049,11 +1049,12 @@ struct TileCone {
     bool ok;
 };
 
-__device__ TileCone tile_cone(const RenderParams &P, int tx, int ty)
+/* the cone of the pixel rectangle [x0, x1] x [r0, r1] (launch rows) */
+__device__ TileCone rect_cone(const RenderParams &P, int x0, int x1, int r0, int r1)
 {
     TileCone K;
-    const int x0 = tx * 8, x1 = min(tx * 8 + 7, P.width - 1);
-    const int r0 = ty * 8, r1 = min(ty * 8 + 7, P.rows - 1);
+    x1 = min(x1, P.width - 1);
+    r1 = min(r1, P.rows - 1);
     const int y0 = P.rowStart + r0 * P.rowStride, y1 = P.rowStart + r1 * P.rowStride;
     /* the same f32 expressions as primary_dir */
     const float dxs[2] = {(float)(x0 - P.width / 2) / (float)(P.height / 2),
@@ -1087,6 +1088,11 @@ __device__ TileCone tile_cone(const RenderParams &P, int tx, int ty)
                            fabs(P.ez.x) <= 1.0001f && fabs(P.ez.y) <= 1.0001f && fabs(P.ez.z) <= 1.0001f;
     K.ok = finite && unitBasis && K.vmin > 1e-6 && K.eDir < 1e-3 && S - S == 0.0;
     return K;
+}
+
+__device__ TileCone tile_cone(const RenderParams &P, int tx, int ty)
+{
+    return rect_cone(P, tx * 8, tx * 8 + 7, ty * 8, ty * 8 + 7);
 }
 
 /* [LB, UB] of g.v/|v| over the tile (see TileCone) */
@@ -1136,25 +1142,46 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
                                                        unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
                                                        unsigned long long *__restrict__ pixMask)
 {
-    __shared__ unsigned wgWeight;
-    if (threadIdx.x == 0)
+    __shared__ unsigned wgWeight, wgAny;
+    extern __shared__ unsigned long long sBlockCand[]; /* maskWords: the block's 16x16 prefilter survivors */
+    if (threadIdx.x == 0) {
         wgWeight = 0;
-    __syncthreads();
+        wgAny = 0;
+    }
     const int bx = blockIdx.x, by = blockIdx.y;
-    const PixelRay px = pixel_ray(P, bx, by);
-    const int lane = threadIdx.x & 63;
-    const int tile = wave_tile(bx, by);
-    unsigned long long *out = mask + (size_t)tile * P.maskWords;
-    bool anyCand = false;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #ifndef RTC_TILE_PREFILTER
 #define RTC_TILE_PREFILTER 1
 #endif
-    const TileCone K = tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2));
+    /* level 1: the prefilter over the workgroup's 16x16 pixels (a superset of each tile's direction range, so
+     * a triangle it prunes fails for every pixel of the four tiles); the waves share the mask words */
+    {
+        const TileCone KB = rect_cone(P, bx * kTileW, bx * kTileW + kTileW - 1, by * kTileH, by * kTileH + kTileH - 1);
+        __syncthreads();
+        for (int w = wave; w < P.maskWords; w += kBlock / 64) {
+            const int ti = w * 64 + lane;
+            const bool maybe = ti < P.triPadded && (!RTC_TILE_PREFILTER || !KB.ok || !tile_prunes(KB, P.primF[ti]));
+            const unsigned long long m = __ballot(maybe);
+            if (lane == 0) {
+                sBlockCand[w] = m;
+                if (m)
+                    wgAny = 1; /* benign race: every writer stores 1 */
+            }
+        }
+        __syncthreads();
+    }
+    const PixelRay px = pixel_ray(P, bx, by);
+    const int tile = wave_tile(bx, by);
+    unsigned long long *out = mask + (size_t)tile * P.maskWords;
+    bool anyCand = false;
+    /* level 2: the tile's own prefilter on the block's survivors, then the per-pixel filter */
+    const TileCone K = wgAny ? tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2)) : TileCone{};
     for (int w = 0; w < P.maskWords; ++w) {
         /* lane l: may triangle 64w + l pass for some pixel of the tile? */
         const int ti = w * 64 + lane;
-        const bool maybe = ti < P.triPadded && (!RTC_TILE_PREFILTER || !K.ok || !tile_prunes(K, P.primF[ti]));
-        unsigned long long todo = __ballot(maybe);
+        const unsigned long long bc = sBlockCand[w];
+        const bool maybe = ((bc >> lane) & 1ull) && (!RTC_TILE_PREFILTER || !K.ok || !tile_prunes(K, P.primF[ti]));
+        unsigned long long todo = bc ? __ballot(maybe) : 0ull;
         unsigned long long bits = 0;
         while (todo) {
             const int j = __builtin_ctzll(todo);
@@ -3297,7 +3324,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * reading the old buffer has finished) */
     const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
     /* (a scene without triangles culls too: every tile is then a sky tile) */
-    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL);
+    /* the tile cull keeps the workgroup's prefilter survivors in LDS (maskWords u64, <= 48 KB: 393,216 triangles);
+     * larger scenes render without it (same frame) */
+    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords <= 6144;
     /* the split launch: every scene for rtc_render_chain, up to kCoopMaxTris triangles for the older heavy
      * kernels (their scene records live in LDS) */
     const int forcedHeavy = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
@@ -3365,7 +3394,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
                            s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, P.geoCount);
     if (cull) {
-        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), 0, st, P, mask, weight, tileW, pixMask);
+        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st, P,
+                           mask, weight, tileW, pixMask);
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {
