@@ -162,8 +162,9 @@ int rtc_rows_selected(const RtcRenderDesc *d);
 /* Per-kernel timing of the split launch: with rtc_scene_set_timing(s, 1) every later launch on s records HIP
  * events around its two kernels (off by default: the records cost each launch a few microseconds), and
  * rtc_scene_kernel_times returns the device times (ms) of the last launch: out[0] the geometry-pixel kernel
- * (rtc_render_chain by default, without the rtc_accumulate_samples pass that follows it), out[1] the sky kernel (concurrent, on the scene's side stream); -1 when that launch recorded none.  Waits
- * for that launch to finish. */
+ * (rtc_render_chain by default, without the rtc_accumulate_samples pass that follows it), out[1] the sky
+ * kernel (concurrent, on the scene's side stream); -1 when that launch recorded none.  Waits for that launch
+ * to finish. */
 int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,

@@ -34,6 +34,12 @@ for k in kernels:
     if c.get("SQ_WAVE_CYCLES"):
         d["_active_valu_over_wave_cycles"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
         d["_wait_inst_any_over_wave_cycles"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
-    d["_dispatches"] = len(disp[k])
+    # dispatches per counter pass (each pass is its own run over the same renders; counters of one pass are
+    # totals over that pass's dispatches)
+    per_file = collections.Counter(f for f, _ in disp[k])
+    n = max(per_file.values()) if per_file else 0
+    d["_dispatches_per_pass"] = n
+    if n:
+        d["_per_dispatch"] = {c: v / n for c, v in sorted(c.items())}
     out[k] = d
 print(json.dumps(out, indent=1))
