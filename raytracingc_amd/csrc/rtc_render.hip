@@ -528,6 +528,11 @@ extern "C" int rtc_rows_selected(const RtcRenderDesc *d)
 }
 
 /* ---- the render kernel ---------------------------------------------------------------------------- */
+/* one deferred sample: radiance * (1/spp), 12 B (stored and read as 3 dwords) */
+struct SampleSlot {
+    float x, y, z;
+};
+
 struct RenderParams {
     const DevTri *__restrict__ tris;
     const DevMat *__restrict__ mats;
@@ -553,7 +558,7 @@ struct RenderParams {
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
-    float4 *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
+    SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
     int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
     unsigned char *__restrict__ colors;
@@ -2711,6 +2716,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
+    __shared__ int sWork; /* the workgroup's next item (see below) */
+    if (threadIdx.x == 0)
+        sWork = 0;
     /* the clustered scene records (clusterCount * 8; pad0 = reference index), staged in LDS up to one chunk */
     DevTri *sRec = MULTI ? nullptr : (DevTri *)sDyn;
     sPow.fill(threadIdx.x);
@@ -2726,17 +2734,22 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     const int lane = threadIdx.x & 63;
     ChainWaveLds &W = sWave[threadIdx.x >> 6];
     const RngJump laneJump = rng_jump_by(7u * (unsigned)lane); /* s -> the state 7 lane draws later */
-    const int nWaves = (int)gridDim.x * (kChainBlock / 64);
-    const int gw = __builtin_amdgcn_readfirstlane((int)blockIdx.x * (kChainBlock / 64) + (int)(threadIdx.x >> 6));
     /* the geometry pixels: kGeoLists sub-lists from rtc_tile_cull, taken as one concatenated index space
-     * (l: the sub-list of item `it`, base: its first item, cnt: its length) */
+     * (l: the sub-list of item `it`, base: its first item, cnt: its length).  Workgroup b owns the items
+     * b + k * gridDim.x; its waves take the next k from an LDS counter, so a wave that drew cheap pixels takes
+     * more of them (a global counter would serialise ~80 k same-address atomics across the XCDs).  A wave's
+     * items increase, as the sub-list walk needs. */
+    int nextIt = 0;
+    if (lane == 0)
+        nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
     const int tilesX = P.blocksX * 2;
     unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segSpec = 0, segClusters = 0;
 #ifdef RTC_DIAG
     unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
 #endif
     int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
-    for (int it = gw;; it += nWaves) {
+    for (;;) {
+        const int it = __builtin_amdgcn_readfirstlane(nextIt);
         while (it - base >= cnt && l < kGeoLists - 1) {
             base += cnt;
             ++l;
@@ -2744,6 +2757,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
         if (it - base >= cnt)
             break;
+        if (lane == 0)
+            nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
         const int code = __builtin_amdgcn_readfirstlane(P.geoList[(size_t)l * P.geoCap + (it - base)]);
         const int tile = code >> 6, bit = code & 63;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
@@ -2857,8 +2872,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             if (deferred) {
                 /* membership only: member lane b of sample index kk stores t at [item][kk]; rtc_accumulate_samples
                  * adds them in sample order */
-                float4 *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
-                const float4 tv = make_float4(t.x, t.y, t.z, 0.f);
+                SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+                const SampleSlot tv{t.x, t.y, t.z};
                 while (k < P.spp && p < nAct) {
                     const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
                     const unsigned long long notOne = ~ones & win;
@@ -2875,9 +2890,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
                     const int hq = __builtin_amdgcn_readlane((int)hits, q);
                     if (hq == 0) { /* the primary ray misses: every remaining sample is this one (no draws) */
-                        const float4 vq = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q)),
-                                                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q)),
-                                                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q)), 0.f);
+                        const SampleSlot vq{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q)),
+                                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q)),
+                                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q))};
                         for (int kk = k + lane; kk < P.spp; kk += 64)
                             slot[kk] = vq;
                         mult += lane == q ? (unsigned)(P.spp - k) : 0u;
@@ -2978,13 +2993,13 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
         items += P.geoCount[l * kGeoCountStride];
     items = min(items, P.sampleCap);
     for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
-        const float4 *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+        const SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
         f2 accxy{0.f, 0.f};
         float accz = 0.f;
         if (P.maxBounce > 0) {
 #pragma unroll 8
             for (int k = 0; k < P.spp; ++k) {
-                const float4 v = slot[k];
+                const SampleSlot v = slot[k];
                 accxy = accxy + f2{v.x, v.y};
                 accz = accz + v.z;
             }
@@ -3373,7 +3388,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result) */
         if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE)) {
-            const size_t per = (size_t)d->spp * sizeof(float4) + sizeof(int);
+            const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
             if (need > s->samplesCap) {
@@ -3385,8 +3400,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipMalloc(&ms->samples, need));
                 ms->samplesCap = need;
             }
-            P.sampleBuf = (float4 *)s->samples;
-            P.itemPix = (int *)(s->samples + cap * (size_t)d->spp * sizeof(float4));
+            P.sampleBuf = (SampleSlot *)s->samples;
+            P.itemPix = (int *)(s->samples + cap * (size_t)d->spp * sizeof(SampleSlot));
             P.sampleCap = (int)cap;
         }
     }
