@@ -2492,7 +2492,10 @@ __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
  * Work: one wave per geometry pixel (rtc_pixel_list), statically strided over a fixed grid (no atomics). */
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
 constexpr int kChainBlock = 256;
-constexpr int kChainWorkers = 2048;
+#ifndef RTC_CHAIN_WORKERS
+#define RTC_CHAIN_WORKERS 1024 /* = the resident capacity (4 workgroups per CU): no second round of workgroups */
+#endif
+constexpr int kChainWorkers = RTC_CHAIN_WORKERS;
 #ifndef RTC_CHAIN_UNROLL
 #define RTC_CHAIN_UNROLL 2
 #endif
