@@ -1160,9 +1160,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 #endif
     /* level 1: the prefilter over the workgroup's 16x16 pixels (a superset of each tile's direction range, so
      * a triangle it prunes fails for every pixel of the four tiles); the waves share the mask words */
-    {
+    __syncthreads();
+    if (wave < P.maskWords) { /* wave-uniform: only the waves with mask words need the block's cone */
         const TileCone KB = rect_cone(P, bx * kTileW, bx * kTileW + kTileW - 1, by * kTileH, by * kTileH + kTileH - 1);
-        __syncthreads();
         for (int w = wave; w < P.maskWords; w += kBlock / 64) {
             const int ti = w * 64 + lane;
             const bool maybe = ti < P.triPadded && (!RTC_TILE_PREFILTER || !KB.ok || !tile_prunes(KB, P.primF[ti]));
@@ -1173,14 +1173,25 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
                     wgAny = 1; /* benign race: every writer stores 1 */
             }
         }
-        __syncthreads();
     }
-    const PixelRay px = pixel_ray(P, bx, by);
+    __syncthreads();
     const int tile = wave_tile(bx, by);
     unsigned long long *out = mask + (size_t)tile * P.maskWords;
+    if (!wgAny) { /* workgroup-uniform: no triangle survives for any of its pixels (most of a sky-heavy frame) */
+        for (int w = lane; w < P.maskWords; w += 64)
+            out[w] = 0ull;
+        if (lane == 0) {
+            tileW[tile] = 0u;
+            pixMask[tile] = 0ull;
+        }
+        if (threadIdx.x == 0)
+            weight[blockIdx.y * gridDim.x + blockIdx.x] = 0u;
+        return;
+    }
+    const PixelRay px = pixel_ray(P, bx, by);
     bool anyCand = false;
     /* level 2: the tile's own prefilter on the block's survivors, then the per-pixel filter */
-    const TileCone K = wgAny ? tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2)) : TileCone{};
+    const TileCone K = tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2));
     for (int w = 0; w < P.maskWords; ++w) {
         /* lane l: may triangle 64w + l pass for some pixel of the tile? */
         const int ti = w * 64 + lane;

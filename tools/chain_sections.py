@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Section cycles of rtc_render_chain from the diagnostic build (librtc_diag.so, s_memtime stamps summed over
-waves), on the BASELINE frame.  Not part of the product."""
+waves), on the BASELINE frame (or another scene: chain_sections.py fsuzane).  Not part of the product."""
 import ctypes as C
 import json
 import os
@@ -13,7 +13,8 @@ os.environ["RTC_LIB_PATH"] = os.path.join(REPO, "raytracingc_amd", "_lib", "libr
 import raytracingc_amd as rt  # noqa: E402
 from conftest import load_tris  # noqa: E402
 
-tris, _ = load_tris("ultracomplex")
+scene_name = sys.argv[1] if len(sys.argv) > 1 else "ultracomplex"
+tris, _ = load_tris(scene_name)
 L = rt.lib()
 L.rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
 out = (C.c_ulonglong * 16)()

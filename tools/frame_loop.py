@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Back-to-back device-resident frames of the BASELINE workload (no D2H), for rocprofv3 kernel traces of the
+launch sequence and its gaps.  Not part of the product.  Usage: frame_loop.py [frames] [hoist]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import torch  # noqa: E402
+
+import raytracingc_amd as rt  # noqa: E402
+from conftest import load_tris  # noqa: E402
+
+frames = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+hoist = len(sys.argv) > 2 and sys.argv[2] == "hoist"
+tris, _ = load_tris("ultracomplex")
+ds = rt.DeviceScene(tris, None)
+cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist)
+out = torch.zeros((1080, 1920, 3), dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream()
+sc, cam = rt.default_scene(), rt.camera_basis()
+for _ in range(frames):
+    ds.render_rows_async(sc, cam, cfg, out.data_ptr(), None, None, st.cuda_stream)
+torch.cuda.synchronize()
+print("frames", frames)
