@@ -561,6 +561,7 @@ struct RenderParams {
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
     int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
+    int chainPrimF;                 /* rtc_render_chain stages DevPrimF[triPadded] in LDS */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
@@ -868,6 +869,24 @@ __device__ __forceinline__ void closest_primary_listed(const RenderParams &P, V3
             const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
             primary_test(P, dir, P.primF[t], t, base, c);
+        }
+    }
+}
+
+/* closest_primary_listed with the DevPrimF records staged in LDS (rtc_render_chain): the filter's record
+ * is an LDS read instead of a dependent scalar load per candidate; DevPrimX (survivors only) stays global. */
+__device__ __forceinline__ void closest_primary_listed_sf(const RenderParams &P, V3 dir, Closest &c,
+                                                          const unsigned long long *__restrict__ mask,
+                                                          const DevPrimF *__restrict__ sF)
+{
+    for (int w = 0; w < P.maskWords; ++w) {
+        unsigned long long m = mask[w];
+        while (m) {
+            const int t = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const DevPrimF &F = sF[t];
+            if (!prim_backfacing(dir, F) && prim_pass(dir, F))
+                primary_exact(P, dir, F, t, 0, c);
         }
     }
 }
@@ -2541,6 +2560,10 @@ struct ChainWaveLds {
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
 static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
+/* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
+ * that keeps 4 blocks (16 waves) per CU */
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
+constexpr size_t kChainLdsBudget = 160 * 1024 / 4;
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records -- or, with
  * ONE, a (lane, record) pair; the owner's ray from LDS, the exact-safe filter, the reference arithmetic for
@@ -2735,10 +2758,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         sWork = 0;
     /* the clustered scene records (clusterCount * 8; pad0 = reference index), staged in LDS up to one chunk */
     DevTri *sRec = MULTI ? nullptr : (DevTri *)sDyn;
+    /* the primary filter records after them, when they fit the block's LDS budget (chainPrimF) */
+    DevPrimF *sPrimF = (!MULTI && P.chainPrimF) ? (DevPrimF *)(sRec + P.clusterCount * kClusterSize) : nullptr;
     sPow.fill(threadIdx.x);
     if (!MULTI)
         for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
             sRec[i] = P.clTris[i];
+    if (sPrimF)
+        for (int i = threadIdx.x; i < P.triPadded; i += kChainBlock)
+            sPrimF[i] = P.primF[i];
 #ifdef RTC_DIAG
     if ((threadIdx.x & 63) < 8)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
@@ -2786,7 +2814,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            closest_primary_listed(P, pdir, prim, 0, mask);
+            if (sPrimF)
+                closest_primary_listed_sf(P, pdir, prim, mask, sPrimF);
+            else
+                closest_primary_listed(P, pdir, prim, 0, mask);
             if (lane == 0) {
                 segTraced++;
                 segTests += L;
@@ -2827,7 +2858,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            closest_primary_listed(P, dir, c, 0, mask);
+                            if (sPrimF)
+                                closest_primary_listed_sf(P, dir, c, mask, sPrimF);
+                            else
+                                closest_primary_listed(P, dir, c, 0, mask);
                             tests += L;
                         }
                     }
@@ -3466,9 +3500,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const bool eight = forced == RTC_F_COOP8;
             const bool pipe = forced == RTC_F_PIPE;
             if (chain) {
-                if (s->chunkCount <= 1)
+                if (s->chunkCount <= 1) {
+                    /* the primary filter records join the staged cluster records when the block still fits 4
+                     * per CU */
+                    const size_t rec = (size_t)s->clusterCount * kClusterSize * sizeof(DevTri);
+                    const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
+                    P.chainPrimF = kChainStaticLds + rec + pf <= kChainLdsBudget;
                     hipLaunchKernelGGL(rtc_render_chain<false>, dim3(kChainWorkers), dim3(kChainBlock),
-                                       (size_t)s->clusterCount * kClusterSize * sizeof(DevTri), st, P);
+                                       rec + (P.chainPrimF ? pf : 0), st, P);
+                }
                 else
                     hipLaunchKernelGGL(rtc_render_chain<true>, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
                 HIP_TRY(hipGetLastError());
