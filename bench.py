@@ -195,7 +195,9 @@ def main():
     ds = rt.DeviceScene(tris, None, device=local)
     seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device=dev)
     rows = rows_per_rank(H, world)
-    stream = torch.cuda.current_stream(dev)
+    # the frames render on a non-blocking stream of their own (not the legacy default stream, whose implicit
+    # synchronisation with other streams costs the overlapped D2H); the copies on a second one
+    stream = torch.cuda.Stream(dev)
     copy_stream = torch.cuda.Stream(dev)
     part = torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) if world > 1 else None
     gathered = torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
@@ -203,41 +205,66 @@ def main():
     frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
     host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
 
-    def frame_step(cfg, b, d2h=True):
-        """One frame into device frame buffer b (rank 0), then its D2H into pinned host buffer b."""
+    # the library records geo_ev on the render stream once a frame's geometry-pixel kernels are enqueued
+    # (rtc_scene_set_geometry_event): the previous frame's D2H starts there, overlapping this frame's sky pass
+    # rather than the start of its persistent geometry kernel (a blit kernel holding CU slots then would delay
+    # some of that kernel's workgroups for the whole copy)
+    geo_ev = torch.cuda.Event()
+    geo_ev.record(stream)
+    torch.cuda.synchronize(dev)
+    ds.set_geometry_event(geo_ev.cuda_event)
+
+    def render_step(cfg, b, count=False):
+        """One frame into device frame buffer b (rank 0: rendered, or gathered and re-interleaved).  count: the
+        kernels also add into the segment counters (instrumentation: a separate untimed frame)."""
         cfg_r = rank_config(cfg, rank, world)
+        segp = seg.data_ptr() if count else None
         if world == 1:
-            ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
+            ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, segp, stream.cuda_stream)
         else:
-            ds.render_rows_async(scene, cam, cfg_r, part.data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
-            dist.gather(part, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(), stream.cuda_stream)
-        if rank == 0 and d2h:
-            ready = torch.cuda.Event()
-            ready.record(stream)
-            copy_stream.wait_event(ready)
-            with torch.cuda.stream(copy_stream):
-                host[b].copy_(frames[b], non_blocking=True)
-            done = torch.cuda.Event()
-            done.record(copy_stream)
-            return done
-        return None
+            with torch.cuda.stream(stream):  # the gather (RCCL) orders itself after the render on this stream
+                ds.render_rows_async(scene, cam, cfg_r, part.data_ptr(), None, segp, stream.cuda_stream)
+                dist.gather(part, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+                if rank == 0:
+                    rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(),
+                                          stream.cuda_stream)
+
+    def d2h_step(b, after):
+        """The D2H of frame buffer b into pinned host buffer b on the copy stream, after event `after`."""
+        copy_stream.wait_event(after)
+        with torch.cuda.stream(copy_stream):
+            host[b].copy_(frames[b], non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(copy_stream)
+        return done
 
     def run(cfg, steps, warmup, d2h=True):
+        """warmup + steps frames; the timed region spans the steps frames, each rendered and (rank 0, d2h) copied
+        into pinned host memory: frame k's D2H overlaps frame k+1's sky pass, the last one is waited for."""
         copied = [None] * nbuf
-        for k in range(warmup):
-            frame_step(cfg, k % nbuf, d2h)
+
+        def frames_loop(n):
+            pending = None
+            for k in range(n):
+                b = k % nbuf
+                if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
+                    stream.wait_event(copied[b])
+                render_step(cfg, b)
+                if rank == 0 and d2h:
+                    if pending is not None:
+                        copied[pending] = d2h_step(pending, geo_ev)
+                    pending = b
+            if rank == 0 and d2h and pending is not None:
+                ready = torch.cuda.Event()
+                ready.record(stream)
+                copied[pending] = d2h_step(pending, ready)
+
+        frames_loop(warmup)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        seg.zero_()
         t0 = time.perf_counter()
-        for k in range(steps):
-            b = k % nbuf
-            if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
-                stream.wait_event(copied[b])
-            copied[b] = frame_step(cfg, b, d2h)
+        frames_loop(steps)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -245,10 +272,14 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # the work counters of one more frame of the same configuration (untimed; every frame is identical)
+        seg.zero_()
+        render_step(cfg, 0, count=True)
+        torch.cuda.synchronize(dev)
         segs = seg.clone()
         if world > 1:
             dist.all_reduce(segs)
-        return float(t[0]), [int(v) // steps for v in segs.tolist()]
+        return float(t[0]), [int(v) for v in segs.tolist()]
 
     cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly))
     # per-kernel device times of the split launch (HIP events the library records around the heavy-tile kernel
@@ -276,7 +307,8 @@ def main():
             ds.render_rows_async(scene, cam, rank_config(cfg, rank, world),
                                  (part if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
             if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
-                host[k % nbuf].copy_(frames[k % nbuf], non_blocking=True)
+                with torch.cuda.stream(stream):
+                    host[k % nbuf].copy_(frames[k % nbuf], non_blocking=True)
         torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -325,7 +357,8 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 ds.render_rows_async(scene, cam, cfg, frames[0].data_ptr(), None, None, stream.cuda_stream)
-                host[0].copy_(frames[0], non_blocking=True)
+                with torch.cuda.stream(stream):
+                    host[0].copy_(frames[0], non_blocking=True)
                 e1.record(stream)
                 e1.synchronize()
                 lat.append(e0.elapsed_time(e1))
@@ -363,7 +396,7 @@ def main():
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
                        "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
-                               "(double-buffered: frame k's D2H overlaps frame k+1's render)",
+                               "(double-buffered: frame k's D2H overlaps frame k+1's sky pass)",
                        "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
                                "environment)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,

@@ -166,6 +166,11 @@ int rtc_rows_selected(const RtcRenderDesc *d);
  * kernel (concurrent, on the scene's side stream); -1 when that launch recorded none.  Waits for that launch
  * to finish. */
 int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
+/* Pipelining hook: every later launch on s records `event` (a caller-created hipEvent_t; NULL stops it) on the
+ * launch's stream once the geometry-pixel kernels are enqueued, before the join with the sky pass; a caller can
+ * start the previous frame's D2H there, so that the copy overlaps the sky pass instead of the next frame's
+ * persistent geometry kernel (whose workgroups then all start at once). */
+int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,

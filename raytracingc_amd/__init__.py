@@ -230,6 +230,13 @@ class DeviceScene:
         """Record HIP events around the split launch's kernels from now on (rtc_scene_set_timing)."""
         check(lib().rtc_scene_set_timing(self._h, int(enable)), "rtc_scene_set_timing")
 
+    def set_geometry_event(self, event_handle: int | None):
+        """From now on every launch records this hipEvent_t (e.g. a torch.cuda.Event's cuda_event) on its stream
+        once the geometry-pixel kernels are enqueued, before the sky pass joins (rtc_scene_set_geometry_event);
+        None stops it."""
+        check(lib().rtc_scene_set_geometry_event(self._h, C.c_void_p(event_handle) if event_handle else None),
+              "rtc_scene_set_geometry_event")
+
     def kernel_times(self):
         """(heavy-tile kernel ms, sky kernel ms) of the last split launch (None if it was not one)."""
         out = (C.c_float * 2)()

@@ -173,6 +173,9 @@ struct RtcDeviceScene {
     hipEvent_t evFork, evJoin;
     /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
     hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
+    /* caller's event (rtc_scene_set_geometry_event): recorded on the caller's stream once a launch's
+     * geometry-pixel kernels are enqueued (before the join with the sky pass); null: none */
+    hipEvent_t geoEvent;
     bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
     bool timed;  /* the last launch was a split launch that recorded them */
 };
@@ -3414,7 +3417,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     }
     P.blocksX = (int)grid.x;
     /* (the counter slots are zero here: rtc_scene_upload clears them, rtc_reduce_segments re-zeroes them) */
+    bool geoRecorded = false;
     auto finish = [&]() -> int {
+        if (s->geoEvent && !geoRecorded)
+            HIP_TRY(hipEventRecord(s->geoEvent, st));
         if (dSegments) {
             hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
             HIP_TRY(hipGetLastError());
@@ -3517,6 +3523,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 if (P.sampleCap > 0) {
                     const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
                     hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
+                }
+                if (s->geoEvent) { /* the geometry pixels are done; the sky pass may still run */
+                    HIP_TRY(hipGetLastError());
+                    HIP_TRY(hipEventRecord(s->geoEvent, st));
+                    geoRecorded = true;
                 }
             }
             else if (spec)
@@ -3865,6 +3876,14 @@ extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const
         rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
     rtc_scene_release(s);
     return rc;
+}
+
+extern "C" int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event)
+{
+    if (!s)
+        return rtc_fail(RTC_EINVAL, "rtc_scene_set_geometry_event: null scene");
+    s->geoEvent = (hipEvent_t)event;
+    return 0;
 }
 
 extern "C" int rtc_scene_set_timing(RtcDeviceScene *s, int enable)
