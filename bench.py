@@ -167,6 +167,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
                     help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
+    ap.add_argument("--d2h-blocks", type=int, default=32,
+                    help="D2H with rtc_copy_async on this many workgroups (0: the runtime's copy)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
     ap.add_argument("--diag-repeat", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -201,7 +203,9 @@ def main():
     copy_stream = torch.cuda.Stream(dev)
     part = torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) if world > 1 else None
     gathered = torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
-    nbuf = 2
+    # three frame buffers: frame k+2 renders while frame k's D2H (issued at frame k+1's geometry-done event) may
+    # still be in flight, so the copy is off the render's critical path
+    nbuf = 3
     frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
     host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
 
@@ -229,11 +233,19 @@ def main():
                     rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(),
                                           stream.cuda_stream)
 
+    def d2h(b, st):
+        """The D2H of frame buffer b into pinned host buffer b on stream st: rtc_copy_async with a few workgroups
+        (--d2h-blocks), or the runtime's copy (a blit kernel with one workgroup per CU) when 0."""
+        if args.d2h_blocks > 0:
+            rt.copy_async(host[b].data_ptr(), frames[b].data_ptr(), frames[b].numel(), args.d2h_blocks, st.cuda_stream)
+        else:
+            with torch.cuda.stream(st):
+                host[b].copy_(frames[b], non_blocking=True)
+
     def d2h_step(b, after):
         """The D2H of frame buffer b into pinned host buffer b on the copy stream, after event `after`."""
         copy_stream.wait_event(after)
-        with torch.cuda.stream(copy_stream):
-            host[b].copy_(frames[b], non_blocking=True)
+        d2h(b, copy_stream)
         done = torch.cuda.Event()
         done.record(copy_stream)
         return done
@@ -307,8 +319,7 @@ def main():
             ds.render_rows_async(scene, cam, rank_config(cfg, rank, world),
                                  (part if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
             if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
-                with torch.cuda.stream(stream):
-                    host[k % nbuf].copy_(frames[k % nbuf], non_blocking=True)
+                d2h(k % nbuf, stream)
         torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -326,11 +337,10 @@ def main():
     d2h_ms = None
     if rank == 0:
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(copy_stream):
-            c0.record(copy_stream)
-            for k in range(10):
-                host[k % nbuf].copy_(frames[k % nbuf], non_blocking=True)
-            c1.record(copy_stream)
+        c0.record(copy_stream)
+        for k in range(10):
+            d2h(k % nbuf, copy_stream)
+        c1.record(copy_stream)
         c1.synchronize()
         d2h_ms = c0.elapsed_time(c1) / 10
 
@@ -357,8 +367,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 ds.render_rows_async(scene, cam, cfg, frames[0].data_ptr(), None, None, stream.cuda_stream)
-                with torch.cuda.stream(stream):
-                    host[0].copy_(frames[0], non_blocking=True)
+                d2h(0, stream)
                 e1.record(stream)
                 e1.synchronize()
                 lat.append(e0.elapsed_time(e1))
@@ -396,7 +405,8 @@ def main():
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
                        "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
-                               "(double-buffered: frame k's D2H overlaps frame k+1's sky pass)",
+                               "(triple-buffered: frame k's D2H, a 32-workgroup copy kernel, overlaps frame k+1's "
+                               "sky pass)",
                        "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
                                "environment)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
@@ -416,6 +426,10 @@ def main():
                                  "kernel time; bruteforce_equiv: segments x T (the reference's brute-force work) per "
                                  "frame time"},
             "frame_ms": round(t / args.steps * 1e3, 4),
+            "d2h_method": (f"rtc_copy_async on {args.d2h_blocks} workgroups" if args.d2h_blocks > 0
+                           else "hipMemcpyAsync (runtime blit kernel)"),
+            "host_frame_equals_device_frame": bool(rank != 0 or torch.equal(torch.from_numpy(host_frame),
+                                                                             frames[(args.steps - 1) % nbuf].cpu())),
             "d2h_ms": round(d2h_ms, 4) if d2h_ms is not None else None,
             "segments_per_frame": seg_calls,
             "segments_traced_per_frame": seg_traced,

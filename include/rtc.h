@@ -175,6 +175,10 @@ int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,
                           unsigned long long *dSegments, void *stream);
+/* Copy `bytes` (16-byte aligned pointers) on `stream` with `blocks` workgroups (<= 0: 32): e.g. Color[] from HBM
+ * into pinned host memory with a small CU footprint while render kernels run (the runtime's D2H blit kernel
+ * takes one workgroup on every CU).  Asynchronous. */
+int rtc_copy_async(void *dst, const void *src, size_t bytes, int blocks, void *stream);
 /* Re-assemble a row-interleaved gather: dCompact holds `parts` blocks of rowsPerPart*width*3 bytes, block
  * g holding rows y = g + k*parts; dOut receives the height*width*3 frame.  Asynchronous on `stream`. */
 int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,

@@ -255,6 +255,12 @@ class DeviceScene:
             pass
 
 
+def copy_async(dst_ptr: int, src_ptr: int, nbytes: int, blocks: int = 32, stream: int | None = None) -> None:
+    """rtc_copy_async: a copy with a small CU footprint (e.g. Color[] into pinned host memory)."""
+    check(lib().rtc_copy_async(C.c_void_p(dst_ptr), C.c_void_p(src_ptr), C.c_size_t(nbytes), int(blocks),
+                               C.c_void_p(stream) if stream else None), "rtc_copy_async")
+
+
 def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,
                        stream: int | None = None):
     check(lib().rtc_deinterleave_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height,

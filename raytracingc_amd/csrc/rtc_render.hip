@@ -3591,6 +3591,47 @@ extern "C" int rtc_deinterleave_async(const void *dCompact, int parts, int rowsP
     return 0;
 }
 
+/* A frame copy with a small footprint (rtc_copy_async): `blocks` workgroups stream 16-byte words (the byte tail
+ * by the first lanes), e.g. from HBM into pinned host memory over PCIe, so a D2H of Color[] occupies a few CU
+ * slots instead of one workgroup on every CU (the runtime's blit kernel) while the render kernels run. */
+__global__ __launch_bounds__(256) void rtc_copy_kernel(const unsigned char *__restrict__ src,
+                                                       unsigned char *__restrict__ dst, size_t bytes)
+{
+    const size_t n16 = bytes / 16;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint4 *s16 = (const uint4 *)src;
+    uint4 *d16 = (uint4 *)dst;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) { /* four independent 16-byte loads in flight per lane */
+        const uint4 a = s16[i], b = s16[i + stride], c = s16[i + 2 * stride], d = s16[i + 3 * stride];
+        d16[i] = a;
+        d16[i + stride] = b;
+        d16[i + 2 * stride] = c;
+        d16[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride)
+        d16[i] = s16[i];
+    const size_t t = n16 * 16 + blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t < bytes)
+        dst[t] = src[t];
+}
+
+extern "C" int rtc_copy_async(void *dst, const void *src, size_t bytes, int blocks, void *stream)
+{
+    if ((!dst || !src) && bytes)
+        return rtc_fail(RTC_EINVAL, "rtc_copy_async: null pointer");
+    if (bytes == 0)
+        return 0;
+    if ((((size_t)dst | (size_t)src) & 15) != 0)
+        return rtc_fail(RTC_EINVAL, "rtc_copy_async: pointers must be 16-byte aligned");
+    if (blocks <= 0)
+        blocks = 32;
+    hipLaunchKernelGGL(rtc_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char *)src, (unsigned char *)dst, bytes);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 /* ---- probes: single reference functions on the device, for known-answer tests ---------------------- */
 __global__ void probe_tri_kernel(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst)
 {

@@ -39,3 +39,15 @@ for flags, name in ((0x0, "hipHostMalloc default"), (0x2, "hipHostMalloc mapped"
     f2 = lambda: hip.hipMemcpyDtoHAsync(hostp, C.c_void_p(src.data_ptr()), C.c_size_t(n), C.c_void_p(st.cuda_stream))
     print(name, "hipMemcpyDtoHAsync ms", round(timed(f2), 4), flush=True)
     hip.hipHostFree(hostp)
+
+# hipMemcpyDeviceToDeviceNoCU (1024): the copy engines (SDMA) instead of a blit kernel, into pinned memory
+src.copy_(torch.arange(n, dtype=torch.int64, device="cuda").to(torch.uint8))
+torch.cuda.synchronize()
+pinned2 = torch.zeros(n, dtype=torch.uint8, pin_memory=True)
+f3 = lambda: hip.hipMemcpyAsync(C.c_void_p(pinned2.data_ptr()), C.c_void_p(src.data_ptr()), C.c_size_t(n), C.c_int(1024),
+                                C.c_void_p(st.cuda_stream))
+rc = f3()
+torch.cuda.synchronize()
+print("NoCU rc", rc, "equal", bool(torch.equal(pinned2, src.cpu())), flush=True)
+if rc == 0:
+    print("torch pinned hipMemcpyAsync NoCU ms", round(timed(f3), 4), flush=True)
