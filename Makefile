@@ -35,7 +35,7 @@ $(BUILD)/rtc_frame.o: $(CSRC)/rtc_frame.hip $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_i
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(BUILD)/rtc_render.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl -L/opt/rocm/lib -lhsa-runtime64
 
 # diagnostic variant (per-wave cycle stamps); never the measured product
 DIAGLIB  := $(LIBDIR)/librtc_diag.so
@@ -43,7 +43,7 @@ $(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/
 	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -c $< -o $@
 
 $(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -ldl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -ldl -L/opt/rocm/lib -lhsa-runtime64
 
 diag: $(DIAGLIB)
 

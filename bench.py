@@ -22,9 +22,11 @@ import argparse
 import json
 import math
 import os
+import queue
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -167,8 +169,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
                     help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
-    ap.add_argument("--d2h-blocks", type=int, default=32,
-                    help="D2H with rtc_copy_async on this many workgroups (0: the runtime's copy)")
+    ap.add_argument("--d2h", default="dma", choices=["dma", "kernel", "runtime"],
+                    help="how Color[] reaches host memory: the SDMA engines (rtc_copy_d2h_dma), a 32-workgroup copy "
+                         "kernel (rtc_copy_async) or hipMemcpyAsync")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
     ap.add_argument("--diag-repeat", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -233,43 +236,89 @@ def main():
                     rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(),
                                           stream.cuda_stream)
 
-    def d2h(b, st):
-        """The D2H of frame buffer b into pinned host buffer b on stream st: rtc_copy_async with a few workgroups
-        (--d2h-blocks), or the runtime's copy (a blit kernel with one workgroup per CU) when 0."""
-        if args.d2h_blocks > 0:
-            rt.copy_async(host[b].data_ptr(), frames[b].data_ptr(), frames[b].numel(), args.d2h_blocks, st.cuda_stream)
+    nbytes = H * W * 3
+
+    def d2h_now(b, st):
+        """The D2H of frame buffer b into pinned host buffer b, ordered after the work enqueued on stream st so
+        far; returns when it is done (dma) or enqueued on st (kernel, runtime)."""
+        if args.d2h == "dma":
+            st.synchronize()
+            rt.copy_d2h_dma(host[b].data_ptr(), frames[b].data_ptr(), nbytes)
+        elif args.d2h == "kernel":
+            rt.copy_async(host[b].data_ptr(), frames[b].data_ptr(), nbytes, 32, st.cuda_stream)
         else:
             with torch.cuda.stream(st):
                 host[b].copy_(frames[b], non_blocking=True)
 
-    def d2h_step(b, after):
-        """The D2H of frame buffer b into pinned host buffer b on the copy stream, after event `after`."""
-        copy_stream.wait_event(after)
-        d2h(b, copy_stream)
-        done = torch.cuda.Event()
-        done.record(copy_stream)
-        return done
-
     def run(cfg, steps, warmup, d2h=True):
         """warmup + steps frames; the timed region spans the steps frames, each rendered and (rank 0, d2h) copied
-        into pinned host memory: frame k's D2H overlaps frame k+1's sky pass, the last one is waited for."""
-        copied = [None] * nbuf
+        into pinned host memory, the copy of frame k overlapping the renders of the next frames:
+          dma     the SDMA engines (rtc_copy_d2h_dma) from a host thread that waits for frame k's event;
+          kernel  a 32-workgroup copy kernel (rtc_copy_async) on a copy stream, from frame k+1's geometry-done
+                  event (rtc_scene_set_geometry_event) so that it overlaps frame k+1's sky pass;
+          runtime hipMemcpyAsync (the runtime's blit kernel), likewise.
+        Frame buffer b is reused only once its previous copy has finished."""
+        use_d2h = d2h and rank == 0
+        if use_d2h and args.d2h == "dma":
+            jobs = queue.Queue()
+            free = [threading.Event() for _ in range(nbuf)]
+            for e in free:
+                e.set()
+            err = []
 
-        def frames_loop(n):
-            pending = None
-            for k in range(n):
-                b = k % nbuf
-                if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
-                    stream.wait_event(copied[b])
-                render_step(cfg, b)
-                if rank == 0 and d2h:
-                    if pending is not None:
-                        copied[pending] = d2h_step(pending, geo_ev)
-                    pending = b
-            if rank == 0 and d2h and pending is not None:
-                ready = torch.cuda.Event()
-                ready.record(stream)
-                copied[pending] = d2h_step(pending, ready)
+            def worker():
+                while True:
+                    job = jobs.get()
+                    if job is None:
+                        return
+                    b, ev = job
+                    try:
+                        ev.synchronize()
+                        rt.copy_d2h_dma(host[b].data_ptr(), frames[b].data_ptr(), nbytes)
+                    except Exception as e:  # surfaced by the main thread
+                        err.append(e)
+                    free[b].set()
+
+            def frames_loop(n):
+                th = threading.Thread(target=worker, daemon=True)
+                th.start()
+                for k in range(n):
+                    b = k % nbuf
+                    free[b].wait()
+                    free[b].clear()
+                    render_step(cfg, b)
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    jobs.put((b, ev))
+                jobs.put(None)
+                th.join()
+                if err:
+                    raise err[0]
+        else:
+            copied = [None] * nbuf
+
+            def copy_after(b, after):
+                copy_stream.wait_event(after)
+                d2h_now(b, copy_stream)
+                done = torch.cuda.Event()
+                done.record(copy_stream)
+                return done
+
+            def frames_loop(n):
+                pending = None
+                for k in range(n):
+                    b = k % nbuf
+                    if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
+                        stream.wait_event(copied[b])
+                    render_step(cfg, b)
+                    if use_d2h:
+                        if pending is not None:
+                            copied[pending] = copy_after(pending, geo_ev)
+                        pending = b
+                if use_d2h and pending is not None:
+                    ready = torch.cuda.Event()
+                    ready.record(stream)
+                    copied[pending] = copy_after(pending, ready)
 
         frames_loop(warmup)
         if world > 1:
@@ -319,7 +368,7 @@ def main():
             ds.render_rows_async(scene, cam, rank_config(cfg, rank, world),
                                  (part if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
             if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
-                d2h(k % nbuf, stream)
+                d2h_now(k % nbuf, stream)
         torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -336,13 +385,12 @@ def main():
     # next frame's render)
     d2h_ms = None
     if rank == 0:
-        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        c0.record(copy_stream)
+        torch.cuda.synchronize(dev)
+        c0 = time.perf_counter()
         for k in range(10):
-            d2h(k % nbuf, copy_stream)
-        c1.record(copy_stream)
-        c1.synchronize()
-        d2h_ms = c0.elapsed_time(c1) / 10
+            d2h_now(k % nbuf, copy_stream)
+        copy_stream.synchronize()
+        d2h_ms = (time.perf_counter() - c0) / 10 * 1e3
 
     extras = {}
     if not args.no_extras:
@@ -364,13 +412,12 @@ def main():
         if rank == 0 and world == 1:
             lat = []
             for _ in range(5):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
+                torch.cuda.synchronize(dev)
+                l0 = time.perf_counter()
                 ds.render_rows_async(scene, cam, cfg, frames[0].data_ptr(), None, None, stream.cuda_stream)
-                d2h(0, stream)
-                e1.record(stream)
-                e1.synchronize()
-                lat.append(e0.elapsed_time(e1))
+                d2h_now(0, stream)
+                stream.synchronize()
+                lat.append((time.perf_counter() - l0) * 1e3)
             extras["frame_latency_ms"] = round(sorted(lat)[len(lat) // 2], 4)
 
     if rank == 0:
@@ -405,8 +452,7 @@ def main():
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
                        "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
-                               "(triple-buffered: frame k's D2H, a 32-workgroup copy kernel, overlaps frame k+1's "
-                               "sky pass)",
+                               "(triple-buffered: frame k's D2H overlaps the next frames' renders; d2h_method)",
                        "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
                                "environment)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
@@ -426,8 +472,9 @@ def main():
                                  "kernel time; bruteforce_equiv: segments x T (the reference's brute-force work) per "
                                  "frame time"},
             "frame_ms": round(t / args.steps * 1e3, 4),
-            "d2h_method": (f"rtc_copy_async on {args.d2h_blocks} workgroups" if args.d2h_blocks > 0
-                           else "hipMemcpyAsync (runtime blit kernel)"),
+            "d2h_method": {"dma": "rtc_copy_d2h_dma (SDMA engines, host copy thread)",
+                           "kernel": "rtc_copy_async (32 workgroups, copy stream)",
+                           "runtime": "hipMemcpyAsync (runtime blit kernel, copy stream)"}[args.d2h],
             "host_frame_equals_device_frame": bool(rank != 0 or torch.equal(torch.from_numpy(host_frame),
                                                                              frames[(args.steps - 1) % nbuf].cpu())),
             "d2h_ms": round(d2h_ms, 4) if d2h_ms is not None else None,

@@ -261,6 +261,11 @@ def copy_async(dst_ptr: int, src_ptr: int, nbytes: int, blocks: int = 32, stream
                                C.c_void_p(stream) if stream else None), "rtc_copy_async")
 
 
+def copy_d2h_dma(host_ptr: int, dev_ptr: int, nbytes: int) -> None:
+    """rtc_copy_d2h_dma: device -> page-locked host memory on the SDMA engines, blocking (GIL released)."""
+    check(lib().rtc_copy_d2h_dma(C.c_void_p(host_ptr), C.c_void_p(dev_ptr), C.c_size_t(nbytes)), "rtc_copy_d2h_dma")
+
+
 def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,
                        stream: int | None = None):
     check(lib().rtc_deinterleave_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height,

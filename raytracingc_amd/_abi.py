@@ -123,7 +123,7 @@ EXPORTS = [
     "rtc_render", "rtc_render_multi",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_scene_set_geometry_event",
-    "rtc_deinterleave_async", "rtc_copy_async",
+    "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
 ]
@@ -176,6 +176,7 @@ def lib() -> C.CDLL:
     L.rtc_scene_set_timing.argtypes = [vp, C.c_int]
     L.rtc_scene_set_geometry_event.argtypes = [vp, vp]
     L.rtc_copy_async.argtypes = [vp, vp, sz, C.c_int, vp]
+    L.rtc_copy_d2h_dma.argtypes = [vp, vp, sz]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]
     L.rtc_render_rows_async.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp,
                                         vp, vp]

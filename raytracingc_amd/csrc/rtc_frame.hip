@@ -366,3 +366,70 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     fill_stats(stats, renderMs, frameMs, seg, d, (size_t)W * H, t0);
     return 0;
 }
+
+/* ---- D2H through the copy engines ------------------------------------------------------------------------
+ * The HIP runtime copies device memory into pinned host memory with a blit kernel (one workgroup per CU); while
+ * render kernels run, those PCIe writes from the shader cores cost the render ~0.1 ms per 1080p frame, even
+ * from a handful of workgroups (tools/copy_overlap_probe.py), whereas the SDMA engines' copy costs it ~0.01 ms
+ * (tools/sdma_overlap_probe.py).  rtc_copy_d2h_dma drives the SDMA engines through the HSA runtime HIP itself
+ * runs on: blocking, for a caller thread that pipelines frame copies behind the renders. */
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <mutex>
+
+namespace {
+struct DmaAgents {
+    std::vector<hsa_agent_t> cpu;
+    bool ok = false;
+};
+DmaAgents &dma_agents()
+{
+    static DmaAgents a;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (hsa_init() != HSA_STATUS_SUCCESS) /* reference-counted: HIP has initialised it already */
+            return;
+        hsa_iterate_agents(
+            [](hsa_agent_t ag, void *p) -> hsa_status_t {
+                hsa_device_type_t t;
+                if (hsa_agent_get_info(ag, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU)
+                    static_cast<DmaAgents *>(p)->cpu.push_back(ag);
+                return HSA_STATUS_SUCCESS;
+            },
+            &a);
+        a.ok = !a.cpu.empty();
+    });
+    return a;
+}
+} // namespace
+
+extern "C" int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes)
+{
+    if ((!hostDst || !devSrc) && bytes)
+        return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: null pointer");
+    if (bytes == 0)
+        return 0;
+    DmaAgents &a = dma_agents();
+    if (!a.ok)
+        return rtc_fail(RTC_ENODEV, "rtc_copy_d2h_dma: no HSA CPU agent");
+    /* the GPU agent that owns the source, and the destination must be page-locked (hipHostMalloc) memory */
+    hsa_amd_pointer_info_t src{}, dst{};
+    src.size = sizeof(src);
+    dst.size = sizeof(dst);
+    if (hsa_amd_pointer_info(devSrc, &src, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        src.type != HSA_EXT_POINTER_TYPE_HSA)
+        return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: source is not device memory");
+    if (hsa_amd_pointer_info(hostDst, &dst, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        (dst.type != HSA_EXT_POINTER_TYPE_HSA && dst.type != HSA_EXT_POINTER_TYPE_LOCKED))
+        return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: destination is not page-locked host memory");
+    thread_local hsa_signal_t sig{0};
+    if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+        return rtc_fail(RTC_ENOMEM, "rtc_copy_d2h_dma: hsa_signal_create failed");
+    hsa_signal_store_screlease(sig, 1);
+    if (hsa_amd_memory_async_copy(hostDst, a.cpu[0], devSrc, src.agentOwner, bytes, 0, nullptr, sig) !=
+        HSA_STATUS_SUCCESS)
+        return rtc_fail(RTC_EIO, "rtc_copy_d2h_dma: hsa_amd_memory_async_copy failed");
+    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    return 0;
+}

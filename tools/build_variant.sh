@@ -10,4 +10,4 @@ mkdir -p /tmp/rtc_variants
   -Rpass-analysis=kernel-resource-usage 2>&1 | grep -A14 "Function Name: _Z16rtc_render_chain" | grep -E "VGPRs:|Spill|Occupancy|Scratch" \
   | sed "s/.*remark: *//;s/ \[.*//" | tr '\n' ' '; echo "<- $name"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC /tmp/rtc_variants/$name.o build/rtc_frame.o build/scene_build.o \
-  -o raytracingc_amd/_lib/librtc_$name.so -ldl
+  -o raytracingc_amd/_lib/librtc_$name.so -ldl -L/opt/rocm/lib -lhsa-runtime64
