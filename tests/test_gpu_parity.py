@@ -508,3 +508,21 @@ def test_cli_bmp_matches_reference(name, tmp_path, gpu_available):
                         "-o", str(tmp_path / "o.bmp")], cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert hashlib.md5((tmp_path / "o.bmp").read_bytes()).hexdigest() == g["bmp_md5"]
+
+
+@pytest.mark.parametrize("nbytes", [1, 15, 4096, 1920 * 1080 * 3 + 7])
+def test_frame_copies(nbytes, gpu_available):
+    """rtc_copy_async (a few workgroups, 16-byte words + byte tail) and rtc_copy_d2h_dma (SDMA engines) deliver
+    the device bytes into pinned host memory exactly."""
+    import torch
+
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+    ref = src.cpu()
+    h1 = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
+    h2 = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
+    st = torch.cuda.current_stream()
+    rt.copy_async(h1.data_ptr(), src.data_ptr(), nbytes, 32, st.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(h1, ref)
+    rt.copy_d2h_dma(h2.data_ptr(), src.data_ptr(), nbytes)
+    assert torch.equal(h2, ref)
