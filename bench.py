@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--d2h", default="dma", choices=["dma", "kernel", "runtime"],
                     help="how Color[] reaches host memory: the SDMA engines (rtc_copy_d2h_dma), a 32-workgroup copy "
                          "kernel (rtc_copy_async) or hipMemcpyAsync")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="join every frame's sky pass into the render stream (no frame pipelining)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
     ap.add_argument("--diag-repeat", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -204,11 +206,14 @@ def main():
     # synchronisation with other streams costs the overlapped D2H); the copies on a second one
     stream = torch.cuda.Stream(dev)
     copy_stream = torch.cuda.Stream(dev)
-    part = torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) if world > 1 else None
-    gathered = torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
+    gather_stream = torch.cuda.Stream(dev)  # N > 1: RCCL gather + re-interleave of each frame, after its render
     # three frame buffers: frame k+2 renders while frame k's D2H (issued at frame k+1's geometry-done event) may
     # still be in flight, so the copy is off the render's critical path
     nbuf = 3
+    parts = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if world > 1 else None
+    gathered = ([torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+                if (world > 1 and rank == 0) else None)
+    part_free = [None] * nbuf  # N > 1: parts[b]'s previous gather has finished
     frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
     host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
 
@@ -222,19 +227,33 @@ def main():
     ds.set_geometry_event(geo_ev.cuda_event)
 
     def render_step(cfg, b, count=False):
-        """One frame into device frame buffer b (rank 0: rendered, or gathered and re-interleaved).  count: the
-        kernels also add into the segment counters (instrumentation: a separate untimed frame)."""
+        """One frame into device frame buffer b (rank 0: rendered, or gathered and re-interleaved); returns the
+        event at which frame buffer b holds the whole frame.  The library records the frame event once both of
+        its passes are written (rtc_scene_set_frame_event: after the join, or with cfg.overlap -- frame
+        pipelining, the next frame's preparation overlapping this one's sky pass -- on its side stream); the
+        gather (RCCL, N > 1) and the D2H wait for it.  count: the kernels also add into the segment counters
+        (instrumentation: a separate untimed frame)."""
         cfg_r = rank_config(cfg, rank, world)
         segp = seg.data_ptr() if count else None
+        ready = torch.cuda.Event()
+        ready.record(stream)  # creates the hipEvent_t (a torch event has none before its first record)
+        ds.set_frame_event(ready.cuda_event)
         if world == 1:
             ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, segp, stream.cuda_stream)
-        else:
-            with torch.cuda.stream(stream):  # the gather (RCCL) orders itself after the render on this stream
-                ds.render_rows_async(scene, cam, cfg_r, part.data_ptr(), None, segp, stream.cuda_stream)
-                dist.gather(part, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-                if rank == 0:
-                    rt.deinterleave_async(gathered.data_ptr(), world, rows, W, H, frames[b].data_ptr(),
-                                          stream.cuda_stream)
+            return ready
+        if part_free[b] is not None:  # parts[b] is rewritten once its previous gather has read it
+            stream.wait_event(part_free[b])
+        ds.render_rows_async(scene, cam, cfg_r, parts[b].data_ptr(), None, segp, stream.cuda_stream)
+        gather_stream.wait_event(ready)
+        with torch.cuda.stream(gather_stream):  # the gather (RCCL) orders itself after the frame on this stream
+            dist.gather(parts[b], gather_list=list(gathered[b].unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                rt.deinterleave_async(gathered[b].data_ptr(), world, rows, W, H, frames[b].data_ptr(),
+                                      gather_stream.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(gather_stream)
+        part_free[b] = done
+        return done
 
     nbytes = H * W * 3
 
@@ -286,10 +305,7 @@ def main():
                     b = k % nbuf
                     free[b].wait()
                     free[b].clear()
-                    render_step(cfg, b)
-                    ev = torch.cuda.Event()
-                    ev.record(stream)
-                    jobs.put((b, ev))
+                    jobs.put((b, render_step(cfg, b)))
                 jobs.put(None)
                 th.join()
                 if err:
@@ -297,8 +313,9 @@ def main():
         else:
             copied = [None] * nbuf
 
-            def copy_after(b, after):
-                copy_stream.wait_event(after)
+            def copy_after(b, *after):
+                for e in after:
+                    copy_stream.wait_event(e)
                 d2h_now(b, copy_stream)
                 done = torch.cuda.Event()
                 done.record(copy_stream)
@@ -310,15 +327,14 @@ def main():
                     b = k % nbuf
                     if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
                         stream.wait_event(copied[b])
-                    render_step(cfg, b)
+                        gather_stream.wait_event(copied[b])
+                    ready = render_step(cfg, b)
                     if use_d2h:
                         if pending is not None:
-                            copied[pending] = copy_after(pending, geo_ev)
-                        pending = b
+                            copied[pending[0]] = copy_after(pending[0], pending[1], geo_ev)
+                        pending = (b, ready)
                 if use_d2h and pending is not None:
-                    ready = torch.cuda.Event()
-                    ready.record(stream)
-                    copied[pending] = copy_after(pending, ready)
+                    copied[pending[0]] = copy_after(pending[0], pending[1])
 
         frames_loop(warmup)
         if world > 1:
@@ -342,15 +358,27 @@ def main():
             dist.all_reduce(segs)
         return float(t[0]), [int(v) for v in segs.tolist()]
 
-    cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly))
-    # per-kernel device times of the split launch (HIP events the library records around the heavy-tile kernel
-    # on this stream and around the sky kernel on the scene's side stream); these untimed frames, and more up to
-    # ~0.3 s, also let the GPU clocks settle before the warmup steps and the timed region
+    # the timed frames are pipelined (RenderConfig.overlap, RTC_F_OVERLAP: frame k+1's preparation overlaps frame
+    # k's sky pass; same frames) unless --no-overlap; the settle, kernel-timing and latency frames are joined
+    cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
+    cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly), overlap=not args.no_overlap)
+    # untimed frames for ~0.3 s: the GPU clocks settle before the kernel timing, the warmup and the timed region
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < 0.3:
+        for k in range(10):
+            ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world),
+                                 (parts[0] if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
+            if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
+                d2h_now(k % nbuf, stream)
+        torch.cuda.synchronize(dev)
+    # per-kernel device times of the split launch (HIP events the library records around the geometry-pixel
+    # kernel on this stream and around the sky kernel on the scene's side stream), averaged over frames rendered
+    # back to back at settled clocks, like rocprofv3's kernel trace of the same command
     heavy_ms = sky_ms = None
     kt = []
     ds.set_timing(True)
-    for _ in range(10):
-        ds.render_rows_async(scene, cam, rank_config(cfg, rank, world), (part if world > 1 else frames[0]).data_ptr(),
+    for _ in range(20):
+        ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world), (parts[0] if world > 1 else frames[0]).data_ptr(),
                              None, None, stream.cuda_stream)
         k = ds.kernel_times()
         if k:
@@ -362,14 +390,6 @@ def main():
         if world > 1:
             dist.all_reduce(hk, op=dist.ReduceOp.MAX)
         heavy_ms, sky_ms = float(hk[0]), float(hk[1])
-    t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < 0.3:
-        for k in range(10):
-            ds.render_rows_async(scene, cam, rank_config(cfg, rank, world),
-                                 (part if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
-            if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
-                d2h_now(k % nbuf, stream)
-        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
 
@@ -399,7 +419,7 @@ def main():
         extras["device_only"] = {"ms_per_step": round(td / args.steps * 1e3, 4),
                                  "value": round(samples * args.steps / td / 1e6, 3)}
         ref_frame = frames[0].clone() if rank == 0 else None
-        th, (_, ht, htests, _, _) = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist=True), args.steps, 1)
+        th, (_, ht, htests, _, _) = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist=True, overlap=cfg.overlap), args.steps, 1)
         extras["hoisted"] = {"value": round(samples * args.steps / th / 1e6, 3),
                              "ms_per_step": round(th / args.steps * 1e3, 4), "segments_traced": ht,
                              "tri_tests": htests,
@@ -414,7 +434,7 @@ def main():
             for _ in range(5):
                 torch.cuda.synchronize(dev)
                 l0 = time.perf_counter()
-                ds.render_rows_async(scene, cam, cfg, frames[0].data_ptr(), None, None, stream.cuda_stream)
+                ds.render_rows_async(scene, cam, cfg_joined, frames[0].data_ptr(), None, None, stream.cuda_stream)
                 d2h_now(0, stream)
                 stream.synchronize()
                 lat.append((time.perf_counter() - l0) * 1e3)
@@ -452,7 +472,10 @@ def main():
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
                        "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
-                               "(triple-buffered: frame k's D2H overlaps the next frames' renders; d2h_method)",
+                               "(triple-buffered: frame k's D2H overlaps the next frames' renders; d2h_method)"
+                               + ("; frames pipelined: frame k+1's primary records and tile cull overlap frame k's "
+                                  "sky pass (RTC_F_OVERLAP), its geometry kernel starts after it" if cfg.overlap else
+                                  "; frames joined (--no-overlap)"),
                        "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
                                "environment)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
@@ -488,7 +511,7 @@ def main():
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             # the GPU's float frame for the bit comparison (one more render through the C ABI)
-            _, gacc, _ = rt.render(tris, None, scene, cam, cfg, device=local, want_accum=True)
+            _, gacc, _ = rt.render(tris, None, scene, cam, cfg_joined, device=local, want_accum=True)
             cb = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_budget_samples, host_frame, gacc)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)

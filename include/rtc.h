@@ -77,6 +77,13 @@ typedef struct RtcRenderDesc {
 #define RTC_F_SPEC          0x100 /* sample-parallel speculation verified in sample order (lanes = samples) */
 #define RTC_F_CHAIN_INLINE  0x400 /* rtc_render_chain adds each pixel's samples itself instead of deferring the
                                      in-order sum to a separate pass (A/B timing; identical frame) */
+#define RTC_F_OVERLAP       0x800 /* frame pipelining (device-resident split only): the launch does not make
+                                     `stream` wait for its sky pass, so the next launch on the same scene prepares
+                                     its frame (primary records, tile cull; double-buffered scratch) while this
+                                     one's sky pass still runs; the next geometry-pixel kernel waits for it.  The
+                                     frame is complete when the scene's frame event (rtc_scene_set_frame_event)
+                                     fires; with segment counters requested the launch joins as usual.  Same
+                                     frame bit for bit. */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render launch (slowest device), HIP events */
@@ -171,6 +178,10 @@ int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
  * start the previous frame's D2H there, so that the copy overlaps the sky pass instead of the next frame's
  * persistent geometry kernel (whose workgroups then all start at once). */
 int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event);
+/* Frame-completion hook: every later launch on s records `event` (NULL stops it) once the whole frame -- the
+ * geometry pixels and the sky pass -- is written: on the launch's stream after the join, or with RTC_F_OVERLAP
+ * (no join) on the scene's side stream after both passes.  Consumers of the frame (a D2H, a gather) wait for it. */
+int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,

@@ -32,6 +32,7 @@ from ._abi import (  # noqa: F401
     RTC_F_NO_COOP,
     RTC_F_PIPE,
     RTC_F_CHAIN_INLINE,
+    RTC_F_OVERLAP,
     RTC_F_SPEC,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
@@ -144,6 +145,9 @@ class RenderConfig:
     spec: bool = False  # the sample-parallel speculative kernel
     pipe: bool = False  # two samples in flight per pixel (faithful only)
     chain_inline: bool = False  # rtc_render_chain sums each pixel's samples itself (no deferred pass)
+    # frame pipelining (DeviceScene.render_rows_async): the launch does not join its sky pass into the stream;
+    # the frame is complete at the scene's frame event (DeviceScene.set_frame_event); same frame
+    overlap: bool = False
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
@@ -151,7 +155,7 @@ class RenderConfig:
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
                 | (RTC_F_COOP4 if self.coop_lanes == 4 else 0) | (RTC_F_COOP8 if self.coop_lanes == 8 else 0)
                 | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe else 0)
-                | (RTC_F_CHAIN_INLINE if self.chain_inline else 0))
+                | (RTC_F_CHAIN_INLINE if self.chain_inline else 0) | (RTC_F_OVERLAP if self.overlap else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
@@ -236,6 +240,13 @@ class DeviceScene:
         None stops it."""
         check(lib().rtc_scene_set_geometry_event(self._h, C.c_void_p(event_handle) if event_handle else None),
               "rtc_scene_set_geometry_event")
+
+    def set_frame_event(self, event_handle: int | None):
+        """From now on every launch records this hipEvent_t once its whole frame is written: on its stream after
+        the join, or with RenderConfig.overlap on the scene's side stream (rtc_scene_set_frame_event); None
+        stops it.  (A torch.cuda.Event has no hipEvent_t before its first record: record it once first.)"""
+        check(lib().rtc_scene_set_frame_event(self._h, C.c_void_p(event_handle) if event_handle else None),
+              "rtc_scene_set_frame_event")
 
     def kernel_times(self):
         """(heavy-tile kernel ms, sky kernel ms) of the last split launch (None if it was not one)."""

@@ -88,6 +88,7 @@ RTC_F_COOP8 = 0x80
 RTC_F_SPEC = 0x100
 RTC_F_PIPE = 0x200
 RTC_F_CHAIN_INLINE = 0x400
+RTC_F_OVERLAP = 0x800
 RTC_SEGMENT_COUNTERS = 5  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
@@ -122,7 +123,7 @@ EXPORTS = [
     "rtc_scene_set_sun", "rtc_camera_basis", "rtc_write_bmp", "rtc_quantize",
     "rtc_render", "rtc_render_multi",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
-    "rtc_scene_set_geometry_event",
+    "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
     "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
@@ -175,6 +176,7 @@ def lib() -> C.CDLL:
     L.rtc_scene_kernel_times.argtypes = [vp, vp]
     L.rtc_scene_set_timing.argtypes = [vp, C.c_int]
     L.rtc_scene_set_geometry_event.argtypes = [vp, vp]
+    L.rtc_scene_set_frame_event.argtypes = [vp, vp]
     L.rtc_copy_async.argtypes = [vp, vp, sz, C.c_int, vp]
     L.rtc_copy_d2h_dma.argtypes = [vp, vp, sz]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]

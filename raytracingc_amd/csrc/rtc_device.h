@@ -63,6 +63,26 @@ __device__ __forceinline__ float smoothstep(float inf, float sup, float x)      
     x = clamp01((x - inf) / (sup - inf));
     return (float)((double)(x * x) * (3.0 - 2.0 * (double)x));
 }
+/* getEnvironmentLight's two smoothsteps (raytracing.c:153 smoothstep(0, .74f, -dir.y), :156
+ * smoothstep(-.01f, 0, -dir.y)) with the f32 divide by the constant sup - inf done as a multiply by its
+ * rounded reciprocal plus one FMA remainder correction (q = n rd, r = n - q d exactly, q + r rd), which is the
+ * correctly rounded n / d here.  n is first limited to [-2, 2] (NaN kept): beyond that the quotient clamps to
+ * the same 0 or 1, and the product cannot overflow.  Bit-identical to smoothstep() for all 2^32 x
+ * (tools/exact_probe.hip). */
+constexpr int kSkyStep = 0, kGroundStep = 1;
+template <int S> __device__ __forceinline__ float smoothstep_k(float x)
+{
+    constexpr float inf = S == kSkyStep ? 0.f : -0.01f;
+    constexpr float sup = S == kSkyStep ? 0.74f : 0.f;
+    constexpr float d = sup - inf;
+    constexpr float rd = 1.f / d;
+    float n = x - inf;
+    n = n > 2.f ? 2.f : n;
+    n = n < -2.f ? -2.f : n;
+    const float q = n * rd;
+    x = clamp01(fmaf(fmaf(-q, d, n), rd, q));
+    return (float)((double)(x * x) * (3.0 - 2.0 * (double)x));
+}
 __device__ __forceinline__ V3 reflect(V3 d, V3 n) { return sub(d, mul(n, 2.f * dot(d, n))); }  /* :79-82; 2*f exact */
 __device__ __forceinline__ V3 lerp(V3 a, V3 b, float t) { return add(mul(a, 1.f - t), mul(b, t)); } /* :84-87 */
 
@@ -214,13 +234,13 @@ __host__ __device__ __forceinline__ bool env_sun_skippable(float focus, float in
  * = +0) -- rays below the horizon --, the sun term as env_sun_skippable says. */
 __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
 {
-    const float skyArg = smoothstep(0.f, 0.74f, -dir.y);
+    const float skyArg = smoothstep_k<kSkyStep>(-dir.y);
     float skyGradientT = 0.f;
     if (__any(__float_as_uint(skyArg) != 0u))
         skyGradientT = pow_ref(skyArg, 0.35f, s);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
     const float sunArg = fmax0_ref(dot(dir, s.sun));
-    float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
+    float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);
     float sunMask = dir.y < 0.f ? 1.f : 0.f;
     float sv = __builtin_copysignf(0.f, s.intensity);
     const bool sunKnown = s.sunSkip && __float_as_uint(sunArg) != 0x80000000u && /* powf(-0, odd) = -0 */

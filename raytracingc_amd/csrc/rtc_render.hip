@@ -162,6 +162,12 @@ struct RtcDeviceScene {
      * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
     unsigned char *scratch;
     size_t scratchCap; /* bytes */
+    /* RTC_F_OVERLAP: launches alternate between two halves of the scratch; skyPending[h]: a sky pass that reads
+     * half h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends) */
+    int flip;
+    bool skyPending[2];
+    hipEvent_t evSkyDone[2], evGeoDone;
+    hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
     /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
      * sample order by rtc_accumulate_samples (grown on demand, <= kSampleBufBudget bytes) */
     unsigned char *samples;
@@ -468,6 +474,9 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
+    for (hipEvent_t *ev : {&s->evSkyDone[0], &s->evSkyDone[1], &s->evGeoDone})
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
         if (e == hipSuccess)
             e = hipEventCreate(ev);
@@ -486,6 +495,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
     int cur = -1;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(s->device);
+    if (s->side) /* an unjoined sky pass (RTC_F_OVERLAP) may still read the scratch */
+        (void)hipStreamSynchronize(s->side);
     if (s->tris)
         (void)hipFree(s->tris);
     if (s->clTris)
@@ -512,7 +523,7 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
         (void)hipEventDestroy(s->evJoin);
-    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1})
+    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evSkyDone[0], s->evSkyDone[1], s->evGeoDone})
         if (ev)
             (void)hipEventDestroy(ev);
     if (s->side)
@@ -1874,7 +1885,7 @@ __device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int gr
 template <int KC>
 __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub)
 {
-    const float sky = smoothstep(0.f, 0.74f, -dir.y);
+    const float sky = smoothstep_k<kSkyStep>(-dir.y);
     const float sunDot = fmax0_ref(dot(dir, s.sun));
     const bool second = (sub & 1) != 0;
     const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f, s);
@@ -1882,7 +1893,7 @@ __device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int s
     const float sunPow = group_lane<KC, 1>(pw, sub);
     const V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
     const float sun = sunPow * s.intensity;
-    const float groundToSkyT = smoothstep(-0.01f, 0.f, -dir.y);
+    const float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);
     const float sunMask = dir.y < 0.f ? 1.f : 0.f;
     const float sv = sun * sunMask;
     return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
@@ -3322,6 +3333,9 @@ static EnvParams env_of(const Scene &s)
 
 __host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
 
+#ifndef RTC_SIDE_STREAM
+#define RTC_SIDE_STREAM 1
+#endif
 extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                                      const RtcRenderDesc *d, void *dColors, float *dAccum,
                                      unsigned long long *dSegments, void *stream)
@@ -3401,18 +3415,30 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64);
+    /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
+     * that counts segments joins, the reduction reads the sky kernel's counters) */
+    const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
+    RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
+    const int half = overlap ? s->flip : 0; /* the scratch half this launch writes */
+    size_t halfBytes = 0;
     if (cull) {
         const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int) +
                             tiles * 64 * sizeof(int) /* + the geometry pixel list */ +
                             (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int); /* + sub-lists */
-        if (need > s->scratchCap) {
-            RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
+        halfBytes = (need + 255) & ~(size_t)255;
+        if (2 * halfBytes > s->scratchCap) { /* both halves (hipFree synchronises the device: no pass still reads them) */
             if (ms->scratch)
                 HIP_TRY(hipFree(ms->scratch));
             ms->scratch = nullptr;
             ms->scratchCap = 0;
-            HIP_TRY(hipMalloc(&ms->scratch, need));
-            ms->scratchCap = need;
+            HIP_TRY(hipMalloc(&ms->scratch, 2 * halfBytes));
+            ms->scratchCap = 2 * halfBytes;
+        }
+        /* an unjoined sky pass of an earlier RTC_F_OVERLAP launch still reading this half: this launch's stream
+         * waits for it before the half is rewritten */
+        if (s->skyPending[half]) {
+            HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[half], 0));
+            ms->skyPending[half] = false;
         }
     }
     P.blocksX = (int)grid.x;
@@ -3425,12 +3451,14 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
             HIP_TRY(hipGetLastError());
         }
+        if (s->frameEvent) /* the whole frame is written once `st` reaches here (joined launches) */
+            HIP_TRY(hipEventRecord(s->frameEvent, st));
         return 0;
     };
     /* the heavy-tile kernel of the split launch: rtc_render_chain unless one of the older ones is forced */
     const int forced = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
     const bool chain = fused && forced == 0;
-    unsigned long long *mask = cull ? (unsigned long long *)s->scratch : nullptr;
+    unsigned long long *mask = cull ? (unsigned long long *)(s->scratch + (size_t)half * halfBytes) : nullptr;
     unsigned long long *pixMask = cull ? mask + tiles * (size_t)s->maskWords : nullptr;
     unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
     unsigned *tileW = cull ? weight + blocks : nullptr;
@@ -3446,7 +3474,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
             if (need > s->samplesCap) {
-                RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
                 if (ms->samples)
                     HIP_TRY(hipFree(ms->samples));
                 ms->samples = nullptr;
@@ -3483,15 +3510,20 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                    heavy, pixList);
                 P.pixList = pixList;
             }
-#ifndef RTC_SIDE_STREAM
-#define RTC_SIDE_STREAM 1
-#endif
             hipStream_t skyStream = RTC_SIDE_STREAM ? s->side : st;
+            /* RTC_F_OVERLAP: the previous launch's sky pass (reading the other scratch half) ends before this
+             * launch's passes start -- its prep and tile cull above overlapped it -- so that the persistent
+             * geometry workgroups all find the chip free and are dispatched first, as in a joined launch (the
+             * fork below follows this wait: a sky pass queued right behind the previous one would otherwise
+             * take the chip first) */
+            if (overlap && s->skyPending[half ^ 1]) {
+                HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[half ^ 1], 0));
+                ms->skyPending[half ^ 1] = false;
+            }
             if (RTC_SIDE_STREAM) {
                 HIP_TRY(hipEventRecord(s->evFork, st));
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
             }
-            RtcDeviceScene *ms = const_cast<RtcDeviceScene *>(s);
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky0, skyStream));
             hipLaunchKernelGGL(rtc_render_sky, grid, dim3(kBlock), 0, skyStream, P, (const unsigned *)tileW);
@@ -3500,6 +3532,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evSky1, skyStream));
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
+            if (overlap) { /* this sky pass reads scratch half `half` until evSkyDone[half] */
+                HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
+                ms->skyPending[half] = true;
+            }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
             const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
@@ -3542,6 +3578,19 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (s->timing && !chain)
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
             ms->timed = s->timing;
+            if (overlap) {
+                /* no join: the frame is complete once the side stream has passed both passes */
+                if (s->geoEvent && !geoRecorded) {
+                    HIP_TRY(hipEventRecord(s->geoEvent, st));
+                    geoRecorded = true;
+                }
+                HIP_TRY(hipEventRecord(s->evGeoDone, st));
+                HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
+                if (s->frameEvent)
+                    HIP_TRY(hipEventRecord(s->frameEvent, s->side));
+                ms->flip ^= 1;
+                return 0;
+            }
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
             return finish();
@@ -3924,6 +3973,14 @@ extern "C" int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event)
     if (!s)
         return rtc_fail(RTC_EINVAL, "rtc_scene_set_geometry_event: null scene");
     s->geoEvent = (hipEvent_t)event;
+    return 0;
+}
+
+extern "C" int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event)
+{
+    if (!s)
+        return rtc_fail(RTC_EINVAL, "rtc_scene_set_frame_event: null scene");
+    s->frameEvent = (hipEvent_t)event;
     return 0;
 }
 

@@ -20,7 +20,7 @@ def test_exact_f32_shortcuts_all_inputs(gpu_available):
     r = subprocess.run([PROBE], capture_output=True, text=True, timeout=100)
     print(r.stdout)
     lines = [ln for ln in r.stdout.splitlines() if "mismatches" in ln]
-    assert len(lines) == 3, r.stdout + r.stderr
+    assert len(lines) == 5, r.stdout + r.stderr
     for ln in lines:
         assert ln.split()[2] == "0", ln
     assert r.returncode == 0

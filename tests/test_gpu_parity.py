@@ -336,6 +336,57 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     ds.close()
 
 
+def test_overlapped_frames_bit_exact(gpu_available):
+    """RTC_F_OVERLAP (frame pipelining): launches that do not join their sky pass, with the next launch's
+    preparation (tile cull into the other scratch half) overlapping it.  Eight frames over three cameras, each
+    consumed (copied) once its frame event fires, and two frames of different cameras into one buffer: every
+    frame equals a joined rtc_render bit for bit."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene = rt.default_scene()
+    cams = [rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1),
+            rt.camera_basis((-5.3, -1.2, -4.1), (1.2, -1.4, 0.7), 0.9)]
+    W, H, spp = 256, 144, 8
+    ref = [rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))[0] for c in cams]
+    cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True)
+    ds = rt.DeviceScene(tris, None)
+    st, cp = torch.cuda.Stream(), torch.cuda.Stream()
+    bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    freed = [None] * 3
+    got = []
+    def new_event():  # a torch event has no hipEvent_t until its first record
+        e = torch.cuda.Event()
+        e.record(st)
+        return e
+
+    for k in range(8):
+        b = k % 3
+        if freed[b] is not None:  # buffer b is rewritten only after its previous frame was copied
+            st.wait_event(freed[b])
+        ev = new_event()
+        ds.set_frame_event(ev.cuda_event)
+        ds.render_rows_async(scene, cams[k % 3], cfg, bufs[b].data_ptr(), stream=st.cuda_stream)
+        cp.wait_event(ev)
+        with torch.cuda.stream(cp):
+            got.append(bufs[b].clone())
+            freed[b] = torch.cuda.Event()
+            freed[b].record(cp)
+    torch.cuda.synchronize()
+    for k, g in enumerate(got):
+        assert np.array_equal(g.cpu().numpy(), ref[k % 3]), f"frame {k}"
+    # one buffer, two cameras back to back: the second frame's geometry pixels are not overwritten by the first
+    # frame's late sky pass
+    ev = new_event()
+    ds.set_frame_event(ev.cuda_event)
+    for c in (cams[1], cams[2]):
+        ds.render_rows_async(scene, c, cfg, bufs[0].data_ptr(), stream=st.cuda_stream)
+    ev.synchronize()
+    assert np.array_equal(bufs[0].cpu().numpy(), ref[2])
+    ds.set_frame_event(None)
+    ds.close()
+
+
 @pytest.mark.parametrize("variant", [{}, {"coop_lanes": 4}, {"coop_lanes": 8}, {"spec": True}, {"hoist": True},
                                      {"pipe": True}, {"chain_inline": True}, {"hoist": True, "chain_inline": True}])
 def test_spp_not_multiple_of_64(variant, gpu_available):

@@ -4,6 +4,8 @@
 //   rcp_cr(x)   == 1.f / x  (IEEE f32 divide)     (normalized(), moremath.c:14; (float)(1./x) == 1.f/x)
 //   powf_glibc_pos(x, y) == powf_glibc(x, y) bit for bit, every x with the sign bit clear, y in kPowY
 //                                                 (getEnvironmentLight's powf, raytracing.c:153,155)
+//   smoothstep_k<S>(x) == smoothstep(inf, sup, x) bit for bit, all 2^32 x, both of getEnvironmentLight's
+//                                                 smoothsteps (raytracing.c:153,156; moremath.c:49-53)
 // Prints one line per check: "<name> mismatches <n> checked <m>".  Exit status 0 iff every count is 0.
 #include <hip/hip_runtime.h>
 
@@ -56,20 +58,45 @@ __global__ void check_pow(unsigned long long base, unsigned long long *bad)
         atomicAdd(&bad[2], (unsigned long long)__popcll(m));
 }
 
+__device__ __forceinline__ float smoothstep_div(float inf, float sup, float x)
+{
+    float d = sup - inf;
+    asm volatile("" : "+v"(d)); /* an IEEE f32 divide, as moremath.c:51 */
+    x = clamp01((x - inf) / d);
+    return (float)((double)(x * x) * (3.0 - 2.0 * (double)x));
+}
+
+__global__ void check_smooth(unsigned long long base, unsigned long long *bad)
+{
+    const unsigned long long i = base + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    const float x = __uint_as_float((unsigned)i);
+    const bool b0 = !same(smoothstep_k<kSkyStep>(x), smoothstep_div(0.f, 0.74f, x));
+    const bool b1 = !same(smoothstep_k<kGroundStep>(x), smoothstep_div(-0.01f, 0.f, x));
+    const unsigned long long m0 = __ballot(b0), m1 = __ballot(b1);
+    if ((threadIdx.x & 63) == 0) {
+        if (m0)
+            atomicAdd(&bad[3], (unsigned long long)__popcll(m0));
+        if (m1)
+            atomicAdd(&bad[4], (unsigned long long)__popcll(m1));
+    }
+}
+
 int main()
 {
     unsigned long long *bad;
-    if (hipMalloc(&bad, 3 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&bad, 5 * sizeof(unsigned long long)) != hipSuccess) {
         printf("no device\n");
         return 2;
     }
-    (void)hipMemset(bad, 0, 3 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 5 * sizeof(unsigned long long));
     const unsigned long long chunk = 1ull << 30;
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
     for (unsigned long long base = 0; base < (1ull << 31); base += chunk)
         hipLaunchKernelGGL(check_pow, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
-    unsigned long long h[3] = {0, 0, 0};
+    for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
+        hipLaunchKernelGGL(check_smooth, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
     if (hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
         printf("copy failed\n");
         return 2;
@@ -77,5 +104,7 @@ int main()
     printf("sqrt_cr mismatches %llu checked %llu\n", h[0], 1ull << 32);
     printf("rcp_cr mismatches %llu checked %llu\n", h[1], 1ull << 32);
     printf("powf_glibc_pos mismatches %llu checked %llu\n", h[2], 8ull << 31);
-    return (h[0] | h[1] | h[2]) ? 1 : 0;
+    printf("smoothstep_sky mismatches %llu checked %llu\n", h[3], 1ull << 32);
+    printf("smoothstep_ground mismatches %llu checked %llu\n", h[4], 1ull << 32);
+    return (h[0] | h[1] | h[2] | h[3] | h[4]) ? 1 : 0;
 }

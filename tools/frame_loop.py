@@ -14,9 +14,10 @@ from conftest import load_tris  # noqa: E402
 
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 hoist = len(sys.argv) > 2 and sys.argv[2] == "hoist"
+overlap = len(sys.argv) > 2 and sys.argv[2] == "overlap"
 tris, _ = load_tris("ultracomplex")
 ds = rt.DeviceScene(tris, None)
-cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist)
+cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist, overlap=overlap)
 out = torch.zeros((1080, 1920, 3), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream()
 sc, cam = rt.default_scene(), rt.camera_basis()
