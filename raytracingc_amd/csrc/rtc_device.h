@@ -164,13 +164,45 @@ __device__ __forceinline__ float random_normal(unsigned &s)
     float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)random_value(s)));
     return (float)((double)rho * rtcmath::cos((double)theta));
 }
-/* RandomDiretion (moremath.c:104-108), components drawn x, y, z */
+/* the exact restatement of three normals (the fallback of random_direction); inlined (out of line, with
+ * RTC_BM_NOINLINE_FALLBACK, the chain kernel spills less but runs ~1.5% slower) */
+#ifdef RTC_BM_NOINLINE_FALLBACK
+__attribute__((noinline))
+#endif
+static __device__ __forceinline__ void random_normals_exact(unsigned &s, float v[3])
+{
+    v[0] = random_normal(s);
+    v[1] = random_normal(s);
+    v[2] = random_normal(s);
+}
+/* RandomDiretion (moremath.c:104-108), components drawn x, y, z.  The three normals take the certified fast
+ * path (rtc_math.h bm_rho_fast / bm_normal_fast: table-driven log and cos, each float returned only when it
+ * provably rounds like the reference's); a lane with any uncertified value (~4e-6 per normal) redraws all three
+ * from the saved state with the exact restatement (random_normal). */
 __device__ __forceinline__ V3 random_direction(unsigned &s)
 {
+#ifndef RTC_EXACT_BM
+    const unsigned s0 = s;
+    float v[3];
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float theta = (float)(2 * 3.14159265 * (double)random_value(s)); /* moremath.c:99 */
+        float rho;
+        ok = rtcmath::bm_rho_fast(random_value(s), rho) && ok;
+        ok = rtcmath::bm_normal_fast(rho, theta, v[c]) && ok;
+    }
+    if (__builtin_expect(!ok, 0)) {
+        s = s0;
+        random_normals_exact(s, v);
+    }
+    return normalized(V3{v[0], v[1], v[2]});
+#else
     float a = random_normal(s);
     float b = random_normal(s);
     float c = random_normal(s);
     return normalized(V3{a, b, c});
+#endif
 }
 
 /* powf for the environment (raytracing.c:153,155): glibc 2.35's own powf algorithm, tables and

@@ -410,6 +410,86 @@ RTC_HD float powf_glibc_pos(float x, float y, const double (*log2tab)[2] = powf_
     return r;
 }
 
+/* ---- certified fast Box-Muller (RandomValueNormalDistrubtion, moremath.c:97-102) -----------------------
+ * The reference's rho = (float)sqrt(-2 log(u)) and n = (float)((double)rho * cos((double)theta)) need glibc's
+ * log and cos only up to the final float rounding.  The fast path evaluates them with short table-driven
+ * schemes (no divide, no branches) and CERTIFIES each float: it is returned only when the double value lies
+ * farther from the float rounding midpoint than the combined error bound of the fast evaluation and of the
+ * reference's own double evaluation (glibc log / cos, double sqrt / product roundings) -- then both round to
+ * the same float.  Otherwise the caller falls back to the exact restatement (log / cos above).  The bounds are
+ * measured exhaustively (tools/check_devmath.cpp: every float u in (0, 1], every float theta in [0, 2 pi]), and
+ * the rho path's final floats are compared with glibc's on every input.
+ *   log: u = 2^k z (glibc's reduction on the float bits), r = z invc - 1 exact (invc a float), log u =
+ *        k ln2 + logc + log1p(r), log1p by a degree-7 polynomial, |r| <= 2^-7;
+ *   cos: theta = j 2pi/64 + t (j * kBmStepHi exact), |t| <= pi/64, cos theta = cos_j cos t - sin_j sin t. */
+#include "rtc_bm_tables.h"
+
+constexpr double kBmLn2Hi = 6.93147180369123816490e-01, kBmLn2Lo = 1.90821492927058770002e-10; /* 43-bit hi */
+constexpr double kBmRhoTol = 0x1p-46; /* relative to rho */
+constexpr double kBmNrmTol = 0x1p-46; /* absolute, per unit rho */
+
+/* half an ulp of a normal float f (exponent field E >= 1), as a double */
+RTC_HD double bm_half_ulp(float f) { return u2d((unsigned long long)(((f2u(f) >> 23) & 0xffu) + 1023u - 151u) << 52); }
+
+/* sqrt(-2 log((double)u)) in double, for u in (0, 1] (the fast scheme, before certification) */
+RTC_HD double bm_rho_d(float u)
+{
+    const unsigned iu = f2u(u);
+    const unsigned tmp = iu - 0x3f330000u;
+    const BmLogEntry e = kBmLogTab[(tmp >> 16) & 127u];
+    const double dk = (double)((int)tmp >> 23);
+    const double r = fma((double)u2f(iu - (tmp & 0xff800000u)), (double)e.invc, -1.0); /* exact */
+    double q = 1.0 / 7.0; /* log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6 + r^5/7) */
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 0.2);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double p = fma(r * r, q, r);
+    const double hi = fma(dk, kBmLn2Hi, e.logcHi);
+    const double lo = fma(dk, kBmLn2Lo, (double)e.logcLo) + p;
+    return __builtin_sqrt(-2.0 * (hi + lo));
+}
+/* rho = (float)sqrt(-2 log((double)u)) for u in (0, 1]; false: not certified (use the exact path) */
+RTC_HD bool bm_rho_fast(float u, float &rho)
+{
+    const double rd = bm_rho_d(u);
+    const float f = (float)rd;
+    rho = f;
+    const double d = fabs(rd - (double)f);
+    return (f2u(f) & 0x7f800000u) != 0u && f2u(u) >= 0x00800000u && d < fma(-rd, kBmRhoTol, bm_half_ulp(f));
+}
+/* cos((double)theta) in double for theta in [0, 2 pi] (the fast scheme) */
+RTC_HD double bm_cos_d(float theta)
+{
+    const double th = (double)theta;
+    const double jd = rint(th * kBmInvStep);
+    double t = fma(-jd, kBmStepHi, th); /* exact */
+    t = fma(-jd, kBmStepLo, t);
+    const double z = t * t;
+    double c = 1.0 / 40320.0; /* cos t = 1 - z/2 + z^2/24 - z^3/720 + z^4/40320 */
+    c = fma(c, z, -1.0 / 720.0);
+    c = fma(c, z, 1.0 / 24.0);
+    c = fma(c, z, -0.5);
+    c = fma(c, z, 1.0);
+    double sn = 1.0 / 362880.0; /* sin t = t (1 - z/6 + z^2/120 - z^3/5040 + z^4/362880) */
+    sn = fma(sn, z, -1.0 / 5040.0);
+    sn = fma(sn, z, 1.0 / 120.0);
+    sn = fma(sn, z, -1.0 / 6.0);
+    sn = fma(sn * z, t, t);
+    const int j = (int)jd & 63;
+    return fma(kBmCosTab[j][0], c, -kBmCosTab[j][1] * sn);
+}
+/* n = (float)((double)rho * cos((double)theta)) for theta = (float)(2 pi u) in [0, 2 pi]; false: not certified */
+RTC_HD bool bm_normal_fast(float rho, float theta, float &n)
+{
+    const double rd = (double)rho * bm_cos_d(theta);
+    const float f = (float)rd;
+    n = f;
+    const double d = fabs(rd - (double)f);
+    return (f2u(f) & 0x7f800000u) != 0u && d < fma(-(double)rho, kBmNrmTol, bm_half_ulp(f));
+}
+
 /* powf(x, y) of raytracing.c:153,155 for x >= 0 (or NaN): exp2(y * log2(x)) in double, rounded once */
 RTC_HD float pow_ref(float x, float y)
 {

@@ -4,7 +4,8 @@ every float theta in [0, 2*pi] for its cos (moremath.c:101), every float x in [0
 155).  The header is the same source the HIP kernel compiles (host and device share IEEE double arithmetic,
 with explicit fma and -ffp-contract=off), so what matters -- the FLOAT results the reference derives -- is
 checked here on the CPU.  This test samples every 251st float; `tools/check_devmath.cpp` with stride 1 is the
-exhaustive run (recorded in DESIGN.md: 0 float mismatches for log and cos over 1.07e9 / 1.09e9 inputs)."""
+exhaustive run (recorded in DESIGN.md: 0 float mismatches for log and cos over 1.07e9 / 1.09e9 inputs; the
+certified fast Box-Muller path: 0 certified floats != glibc over every u, 4e8 random normals)."""
 from __future__ import annotations
 
 import os
@@ -45,5 +46,14 @@ def test_devmath_matches_glibc_where_it_matters(checker):
         assert m and int(m.group(1)) > 4_000_000 and int(m.group(2)) == 0, out
     m = re.search(r"glibc-powf random: (\d+) inputs, fma-build (\d+) != libm", out)
     assert m and int(m.group(2)) == 0, out
+    # the certified fast Box-Muller path: no certified float differs from glibc's, the fast schemes' errors stay
+    # far inside the certification tolerances, and almost every draw is certified
+    m = re.search(r"bm_rho: (\d+) inputs, (\d+) certified, (\d+) certified != glibc, max rel err (\S+) \(tol (\S+)\)", out)
+    assert m and int(m.group(3)) == 0 and int(m.group(2)) >= 0.99 * int(m.group(1)), out
+    assert float(m.group(4)) * 16 <= float(m.group(5)), out
+    m = re.search(r"bm_cos: (\d+) inputs, max abs err (\S+) \(tol (\S+)\)", out)
+    assert m and float(m.group(2)) * 16 <= float(m.group(3)), out
+    m = re.search(r"bm_normal: (\d+) draws, (\d+) certified, (\d+) certified != glibc", out)
+    assert m and int(m.group(3)) == 0 and int(m.group(2)) >= 0.9999 * int(m.group(1)), out
     m = re.search(r"random_value: (\d+) != divide", out)
     assert m and int(m.group(1)) == 0, out

@@ -45,6 +45,54 @@ int main(int argc, char **argv)
             dprod += ((float)((double)r * a) != (float)((double)r * g));
     }
     printf("cos: %lld inputs, %lld double != glibc, %lld float rho*cos != glibc (4 rho each)\n", n2, dcos, dprod);
+    // 2b. the certified fast Box-Muller path (rtc_math.h bm_*): the fast schemes' largest errors against glibc
+    //     (they must stay within the certification tolerances), the rho path's certified floats against glibc's
+    //     on every u, and certified normals on random (u1, u2) draws
+    {
+        long long nr = 0, certR = 0, wrongR = 0;
+        double maxRelRho = 0.0;
+#pragma omp parallel for reduction(+ : nr, certR, wrongR) reduction(max : maxRelRho) schedule(static, 65536)
+        for (long long b = 1; b <= 0x3f800000LL; b += stride) {
+            const float u = f_of((uint32_t)b);
+            const double g = sqrt(-2 * ::log((double)u));
+            const double a = rtcmath::bm_rho_d(u);
+            if (g > 0 && b >= 0x00800000LL) /* normal u (the RNG's are 0 or >= 2^-32) */
+                maxRelRho = fmax(maxRelRho, fabs(a - g) / g);
+            float rho;
+            const bool ok = rtcmath::bm_rho_fast(u, rho);
+            nr++;
+            certR += ok;
+            wrongR += ok && rtcmath::f2u(rho) != rtcmath::f2u((float)g);
+        }
+        printf("bm_rho: %lld inputs, %lld certified, %lld certified != glibc, max rel err %.3g (tol %.3g)\n", nr, certR,
+               wrongR, maxRelRho, rtcmath::kBmRhoTol);
+        long long nc = 0;
+        double maxAbsCos = 0.0;
+#pragma omp parallel for reduction(+ : nc) reduction(max : maxAbsCos) schedule(static, 65536)
+        for (long long b = 0; b <= 0x40c90fdbLL; b += stride) {
+            const float t = f_of((uint32_t)b);
+            nc++;
+            maxAbsCos = fmax(maxAbsCos, fabs(rtcmath::bm_cos_d(t) - ::cos((double)t)));
+        }
+        printf("bm_cos: %lld inputs, max abs err %.3g (tol %.3g)\n", nc, maxAbsCos, rtcmath::kBmNrmTol);
+        long long nn = 0, certN = 0, wrongN = 0;
+#pragma omp parallel for reduction(+ : nn, certN, wrongN) schedule(static, 1 << 16)
+        for (long long k = 0; k < 400000000LL / (long long)stride + 1; ++k) {
+            uint64_t x = (uint64_t)k * 0x9e3779b97f4a7c15ull;
+            x ^= x >> 29, x *= 0xbf58476d1ce4e5b9ull, x ^= x >> 32;
+            const float u1 = (float)fma((double)(uint32_t)x, 0x1p-64, (double)(uint32_t)x * 0x1p-32);
+            const float u2 = (float)fma((double)(uint32_t)(x >> 32), 0x1p-64, (double)(uint32_t)(x >> 32) * 0x1p-32);
+            const float theta = (float)(2 * 3.14159265 * (double)u1);
+            const float rho = (float)sqrt(-2 * ::log((double)u2));
+            const float g = (float)((double)rho * ::cos((double)theta));
+            float n;
+            const bool ok = rtcmath::bm_normal_fast(rho, theta, n);
+            nn++;
+            certN += ok;
+            wrongN += ok && rtcmath::f2u(n) != rtcmath::f2u(g);
+        }
+        printf("bm_normal: %lld draws, %lld certified, %lld certified != glibc\n", nn, certN, wrongN);
+    }
     // 3. powf(x, y) for x in [0, 1] (raytracing.c:153,155)
     const float ys[3] = {0.35f, 22.f, 7.5f};
     for (float y : ys) {
