@@ -4,6 +4,9 @@
 //   rcp_cr(x)   == 1.f / x  (IEEE f32 divide)     (normalized(), moremath.c:14; (float)(1./x) == 1.f/x)
 //   powf_glibc_pos(x, y) == powf_glibc(x, y) bit for bit, every x with the sign bit clear, y in kPowY
 //                                                 (getEnvironmentLight's powf, raytracing.c:153,155)
+//   bm_rho_fast(u) == (float)sqrt(-2 log u) (exact restatement) whenever certified, every float u in (0, 1];
+//   bm_normal_fast(rho, theta) == (float)(rho cos theta) likewise, every float theta in [0, 2 pi] x 4 rho
+//                                                 (the certified fast Box-Muller path, moremath.c:97-102)
 //   smoothstep_k<S>(x) == smoothstep(inf, sup, x) bit for bit, all 2^32 x, both of getEnvironmentLight's
 //                                                 smoothsteps (raytracing.c:153,156; moremath.c:49-53)
 // Prints one line per check: "<name> mismatches <n> checked <m>".  Exit status 0 iff every count is 0.
@@ -81,22 +84,53 @@ __global__ void check_smooth(unsigned long long base, unsigned long long *bad)
     }
 }
 
+__global__ void check_bm(unsigned long long base, unsigned long long *bad)
+{
+    const unsigned long long i = base + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    unsigned b = 0, c = 0;
+    if (i >= 1 && i <= 0x3f800000ull) { /* u in (0, 1] */
+        const float u = __uint_as_float((unsigned)i);
+        float rho;
+        if (rtcmath::bm_rho_fast(u, rho)) {
+            c++;
+            b += __float_as_uint(rho) != __float_as_uint((float)__builtin_sqrt(-2 * rtcmath::log((double)u)));
+        }
+    }
+    if (i <= 0x40c90fdbull) { /* theta in [0, 2 pi] */
+        const float t = __uint_as_float((unsigned)i);
+        const float rhos[4] = {0.37f, 1.0f, 1.7724539f, 3.3f};
+        for (float r : rhos) {
+            float n;
+            if (rtcmath::bm_normal_fast(r, t, n)) {
+                c++;
+                b += __float_as_uint(n) != __float_as_uint((float)((double)r * rtcmath::cos((double)t)));
+            }
+        }
+    }
+    const unsigned long long m = __ballot(b != 0);
+    if ((threadIdx.x & 63) == 0 && m)
+        atomicAdd(&bad[5], (unsigned long long)__popcll(m));
+    (void)c;
+}
+
 int main()
 {
     unsigned long long *bad;
-    if (hipMalloc(&bad, 5 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&bad, 6 * sizeof(unsigned long long)) != hipSuccess) {
         printf("no device\n");
         return 2;
     }
-    (void)hipMemset(bad, 0, 5 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 6 * sizeof(unsigned long long));
     const unsigned long long chunk = 1ull << 30;
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
     for (unsigned long long base = 0; base < (1ull << 31); base += chunk)
         hipLaunchKernelGGL(check_pow, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
+    for (unsigned long long base = 0; base < (1ull << 31); base += chunk)
+        hipLaunchKernelGGL(check_bm, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check_smooth, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
-    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
     if (hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
         printf("copy failed\n");
         return 2;
@@ -106,5 +140,6 @@ int main()
     printf("powf_glibc_pos mismatches %llu checked %llu\n", h[2], 8ull << 31);
     printf("smoothstep_sky mismatches %llu checked %llu\n", h[3], 1ull << 32);
     printf("smoothstep_ground mismatches %llu checked %llu\n", h[4], 1ull << 32);
-    return (h[0] | h[1] | h[2] | h[3] | h[4]) ? 1 : 0;
+    printf("bm_fast mismatches %llu checked %llu\n", h[5], 0x3f800000ull + 4 * 0x40c90fdcull);
+    return (h[0] | h[1] | h[2] | h[3] | h[4] | h[5]) ? 1 : 0;
 }
