@@ -175,6 +175,7 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="join every frame's sky pass into the render stream (no frame pipelining)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
+    ap.add_argument("--force-gather", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--diag-repeat", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -192,8 +193,14 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    # --force-gather: the multi-GPU data path (per-rank parts, RCCL gather on its own stream, re-interleave) with a
+    # single rank -- its streams, events and RCCL calls exercised on a one-GPU box (RCCL refuses two ranks on one
+    # device, so N > 1 itself cannot be rehearsed there)
+    multi = world > 1 or args.force_gather
+    if multi:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     scene_name, W, H, spp = WORKLOADS[args.workload]
     tris, tonly = load_scene(scene_name)
@@ -210,9 +217,9 @@ def main():
     # three frame buffers: frame k+2 renders while frame k's D2H (issued at frame k+1's geometry-done event) may
     # still be in flight, so the copy is off the render's critical path
     nbuf = 3
-    parts = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if world > 1 else None
+    parts = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else None
     gathered = ([torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-                if (world > 1 and rank == 0) else None)
+                if (multi and rank == 0) else None)
     part_free = [None] * nbuf  # N > 1: parts[b]'s previous gather has finished
     frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
     host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
@@ -238,7 +245,7 @@ def main():
         ready = torch.cuda.Event()
         ready.record(stream)  # creates the hipEvent_t (a torch event has none before its first record)
         ds.set_frame_event(ready.cuda_event)
-        if world == 1:
+        if not multi:
             ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, segp, stream.cuda_stream)
             return ready
         if part_free[b] is not None:  # parts[b] is rewritten once its previous gather has read it
@@ -337,24 +344,24 @@ def main():
                     copied[pending[0]] = copy_after(pending[0], pending[1])
 
         frames_loop(warmup)
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         frames_loop(steps)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if multi:
             dist.barrier()
         dt = time.perf_counter() - t0
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        if world > 1:
+        if multi:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         # the work counters of one more frame of the same configuration (untimed; every frame is identical)
         seg.zero_()
         render_step(cfg, 0, count=True)
         torch.cuda.synchronize(dev)
         segs = seg.clone()
-        if world > 1:
+        if multi:
             dist.all_reduce(segs)
         return float(t[0]), [int(v) for v in segs.tolist()]
 
@@ -367,7 +374,7 @@ def main():
     while time.perf_counter() - t_settle < 0.3:
         for k in range(10):
             ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world),
-                                 (parts[0] if world > 1 else frames[0]).data_ptr(), None, None, stream.cuda_stream)
+                                 (parts[0] if multi else frames[0]).data_ptr(), None, None, stream.cuda_stream)
             if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
                 d2h_now(k % nbuf, stream)
         torch.cuda.synchronize(dev)
@@ -378,7 +385,7 @@ def main():
     kt = []
     ds.set_timing(True)
     for _ in range(20):
-        ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world), (parts[0] if world > 1 else frames[0]).data_ptr(),
+        ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world), (parts[0] if multi else frames[0]).data_ptr(),
                              None, None, stream.cuda_stream)
         k = ds.kernel_times()
         if k:
@@ -387,10 +394,10 @@ def main():
     if kt:
         hk = torch.tensor([sum(a for a, _ in kt) / len(kt), sum(b for _, b in kt) / len(kt)], dtype=torch.float64,
                           device=dev)
-        if world > 1:
+        if multi:
             dist.all_reduce(hk, op=dist.ReduceOp.MAX)
         heavy_ms, sky_ms = float(hk[0]), float(hk[1])
-    if world > 1:
+    if multi:
         dist.barrier()
 
     if args.diag_repeat:  # diagnosis only: the same timed run a few times before the reported one
@@ -508,6 +515,10 @@ def main():
             "discarded_tri_tests_per_frame": discarded_tests,
             "gtests_per_s": round(tri_tests * args.steps / t / 1e9, 2),
         }
+        if multi:
+            # the gathered, re-interleaved frame as it landed on the host == one GPU rendering the whole frame
+            ref1, _, _ = rt.render(tris, None, scene, cam, cfg_joined, device=local)
+            line["frame_equals_1gpu_render"] = bool(np.array_equal(host_frame, ref1))
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             # the GPU's float frame for the bit comparison (one more render through the C ABI)
@@ -517,7 +528,7 @@ def main():
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(line), flush=True)
     ds.close()
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
