@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
-"""Device-to-host copy rate of rtc_copy_d2h_dma for a 1080p and a 4K frame, with the SDMA engine count the
-environment chooses (RTC_D2H_ENGINES); checks the bytes.  Not part of the product.  Usage: RTC_D2H_ENGINES=n
-d2h_engines_probe.py
+"""Device-to-host copy rate of rtc_copy_d2h_dma (SDMA) for a 1080p and a 4K frame; checks the bytes.  Not part
+of the product.  Usage: d2h_engines_probe.py
 (r02: one engine already moves ~52-54 GB/s, the PCIe limit: 0.12 ms per 1080p frame, 0.46 ms per 4K frame;
 the split over 2-4 engines measured the same and was not kept)"""
 import json
@@ -15,7 +14,7 @@ import torch  # noqa: E402
 
 import raytracingc_amd as rt  # noqa: E402
 
-out = {"engines": os.environ.get("RTC_D2H_ENGINES", "default")}
+out = {}
 for name, n in (("1080p", 1920 * 1080 * 3), ("4k", 3840 * 2160 * 3)):
     src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
     dst = torch.empty(n, dtype=torch.uint8, pin_memory=True)
