@@ -244,13 +244,17 @@ def main():
         segp = seg.data_ptr() if count else None
         ready = torch.cuda.Event()
         ready.record(stream)  # creates the hipEvent_t (a torch event has none before its first record)
+        # the library records the frame event while enqueuing the launch; it is cleared right after, so that no
+        # later launch records an event this function's caller may already have released
         ds.set_frame_event(ready.cuda_event)
         if not multi:
             ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, segp, stream.cuda_stream)
+            ds.set_frame_event(None)
             return ready
         if part_free[b] is not None:  # parts[b] is rewritten once its previous gather has read it
             stream.wait_event(part_free[b])
         ds.render_rows_async(scene, cam, cfg_r, parts[b].data_ptr(), None, segp, stream.cuda_stream)
+        ds.set_frame_event(None)
         gather_stream.wait_event(ready)
         with torch.cuda.stream(gather_stream):  # the gather (RCCL) orders itself after the frame on this stream
             dist.gather(parts[b], gather_list=list(gathered[b].unbind(0)) if rank == 0 else None, dst=0)

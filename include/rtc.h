@@ -180,7 +180,8 @@ int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
 int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event);
 /* Frame-completion hook: every later launch on s records `event` (NULL stops it) once the whole frame -- the
  * geometry pixels and the sky pass -- is written: on the launch's stream after the join, or with RTC_F_OVERLAP
- * (no join) on the scene's side stream after both passes.  Consumers of the frame (a D2H, a gather) wait for it. */
+ * (no join) on the scene's side stream after both passes.  Consumers of the frame (a D2H, a gather) wait for it.
+ * The event must stay valid while launches record it (set NULL before destroying it). */
 int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,

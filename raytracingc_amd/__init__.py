@@ -244,7 +244,8 @@ class DeviceScene:
     def set_frame_event(self, event_handle: int | None):
         """From now on every launch records this hipEvent_t once its whole frame is written: on its stream after
         the join, or with RenderConfig.overlap on the scene's side stream (rtc_scene_set_frame_event); None
-        stops it.  (A torch.cuda.Event has no hipEvent_t before its first record: record it once first.)"""
+        stops it.  The event must stay alive while launches record it: clear it (None) before releasing it.
+        (A torch.cuda.Event has no hipEvent_t before its first record: record it once first.)"""
         check(lib().rtc_scene_set_frame_event(self._h, C.c_void_p(event_handle) if event_handle else None),
               "rtc_scene_set_frame_event")
 
