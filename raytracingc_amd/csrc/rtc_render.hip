@@ -167,12 +167,6 @@ struct RtcDeviceScene {
     int flip;
     bool skyPending[2];
     hipEvent_t evSkyDone[2], evGeoDone;
-    /* RTC_F_OVERLAP: rtc_accumulate_samples runs on `acc` (from evChainDone), so that the next launch's prep and
-     * tile cull do not queue behind it; accPending: the next geometry kernel (which rewrites the sample slots)
-     * waits for evAccDone */
-    hipStream_t acc;
-    hipEvent_t evChainDone, evAccDone;
-    bool accPending;
     hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
     /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
      * sample order by rtc_accumulate_samples (grown on demand, <= kSampleBufBudget bytes) */
@@ -480,9 +474,7 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&s->acc, hipStreamNonBlocking);
-    for (hipEvent_t *ev : {&s->evSkyDone[0], &s->evSkyDone[1], &s->evGeoDone, &s->evChainDone, &s->evAccDone})
+    for (hipEvent_t *ev : {&s->evSkyDone[0], &s->evSkyDone[1], &s->evGeoDone})
         if (e == hipSuccess)
             e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
@@ -531,10 +523,7 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
         (void)hipEventDestroy(s->evJoin);
-    if (s->acc)
-        (void)hipStreamSynchronize(s->acc);
-    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evSkyDone[0], s->evSkyDone[1], s->evGeoDone,
-                          s->evChainDone, s->evAccDone})
+    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evSkyDone[0], s->evSkyDone[1], s->evGeoDone})
         if (ev)
             (void)hipEventDestroy(ev);
     if (s->side)
@@ -3432,12 +3421,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
     const int half = overlap ? s->flip : 0; /* the scratch half this launch writes */
     size_t halfBytes = 0;
-    /* an earlier RTC_F_OVERLAP launch's in-order sums may still read the sample slots and its scratch half: a
-     * joined launch waits for them first (an overlapped one before its geometry kernel, below) */
-    if (!overlap && s->accPending) {
-        HIP_TRY(hipStreamWaitEvent(st, s->evAccDone, 0));
-        ms->accPending = false;
-    }
     if (cull) {
         const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int) +
                             tiles * 64 * sizeof(int) /* + the geometry pixel list */ +
@@ -3559,10 +3542,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const bool eight = forced == RTC_F_COOP8;
             const bool pipe = forced == RTC_F_PIPE;
             if (chain) {
-                if (overlap && s->accPending) { /* the previous launch's in-order sums still read the sample slots */
-                    HIP_TRY(hipStreamWaitEvent(st, s->evAccDone, 0));
-                    ms->accPending = false;
-                }
                 if (s->chunkCount <= 1) {
                     /* the primary filter records join the staged cluster records when the block still fits 4
                      * per CU */
@@ -3577,26 +3556,14 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipGetLastError());
                 if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                     HIP_TRY(hipEventRecord(s->evHeavy1, st));
-                /* RTC_F_OVERLAP: the in-order sums on the scene's `acc` stream, concurrently with the next launch's
-                 * prep and tile cull on `st` */
-                hipStream_t accStream = st;
-                if (overlap && P.sampleCap > 0) {
-                    HIP_TRY(hipEventRecord(s->evChainDone, st));
-                    HIP_TRY(hipStreamWaitEvent(s->acc, s->evChainDone, 0));
-                    accStream = s->acc;
-                }
                 if (P.sampleCap > 0) {
                     const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                    hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, accStream, P);
+                    hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
                 }
                 if (s->geoEvent) { /* the geometry pixels are done; the sky pass may still run */
                     HIP_TRY(hipGetLastError());
-                    HIP_TRY(hipEventRecord(s->geoEvent, accStream));
+                    HIP_TRY(hipEventRecord(s->geoEvent, st));
                     geoRecorded = true;
-                }
-                if (accStream != st) {
-                    HIP_TRY(hipEventRecord(s->evAccDone, accStream));
-                    ms->accPending = true;
                 }
             }
             else if (spec)
@@ -3617,12 +3584,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                     HIP_TRY(hipEventRecord(s->geoEvent, st));
                     geoRecorded = true;
                 }
-                if (s->accPending) { /* the geometry pixels are complete with the in-order sums */
-                    HIP_TRY(hipStreamWaitEvent(s->side, s->evAccDone, 0));
-                } else {
-                    HIP_TRY(hipEventRecord(s->evGeoDone, st));
-                    HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
-                }
+                HIP_TRY(hipEventRecord(s->evGeoDone, st));
+                HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
                 if (s->frameEvent)
                     HIP_TRY(hipEventRecord(s->frameEvent, s->side));
                 ms->flip ^= 1;
