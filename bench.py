@@ -280,6 +280,8 @@ def main():
             with torch.cuda.stream(st):
                 host[b].copy_(frames[b], non_blocking=True)
 
+    copy_ms = []  # dma: each frame copy's duration as the copying thread saw it (the last run)
+
     def run(cfg, steps, warmup, d2h=True):
         """warmup + steps frames; the timed region spans the steps frames, each rendered and (rank 0, d2h) copied
         into pinned host memory, the copy of frame k overlapping the renders of the next frames:
@@ -289,6 +291,7 @@ def main():
           runtime hipMemcpyAsync (the runtime's blit kernel), likewise.
         Frame buffer b is reused only once its previous copy has finished."""
         use_d2h = d2h and rank == 0
+        copy_ms.clear()
         if use_d2h and args.d2h == "dma":
             jobs = queue.Queue()
             free = [threading.Event() for _ in range(nbuf)]
@@ -304,7 +307,9 @@ def main():
                     b, ev = job
                     try:
                         ev.synchronize()
+                        c0 = time.perf_counter()
                         rt.copy_d2h_dma(host[b].data_ptr(), frames[b].data_ptr(), nbytes)
+                        copy_ms.append((time.perf_counter() - c0) * 1e3)
                     except Exception as e:  # surfaced by the main thread
                         err.append(e)
                     free[b].set()
@@ -412,10 +417,12 @@ def main():
     value = samples * args.steps / t / 1e6
     # the last frame of the timed run as it landed in host memory
     host_frame = host[(args.steps - 1) % nbuf].numpy().copy() if rank == 0 else None
-    # the D2H of one frame on its own (HIP events on the copy stream; inside the timed run it overlaps the
-    # next frame's render)
+    # the D2H of one frame: dma -- the median copy of the timed run (SDMA, overlapping the next frames' renders);
+    # kernel / runtime -- ten copies on their own after it
     d2h_ms = None
-    if rank == 0:
+    if rank == 0 and args.d2h == "dma" and copy_ms:
+        d2h_ms = sorted(copy_ms)[len(copy_ms) // 2]
+    elif rank == 0:
         torch.cuda.synchronize(dev)
         c0 = time.perf_counter()
         for k in range(10):
