@@ -2577,7 +2577,10 @@ static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a fu
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
 constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
-constexpr size_t kChainLdsBudget = 160 * 1024 / 4;
+#ifndef RTC_CHAIN_WGS_PER_CU
+#define RTC_CHAIN_WGS_PER_CU 4
+#endif
+constexpr size_t kChainLdsBudget = 160 * 1024 / RTC_CHAIN_WGS_PER_CU;
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records -- or, with
  * ONE, a (lane, record) pair; the owner's ray from LDS, the exact-safe filter, the reference arithmetic for
