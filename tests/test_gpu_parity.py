@@ -336,11 +336,12 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     ds.close()
 
 
-def test_overlapped_frames_bit_exact(gpu_available):
+@pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}, {"coop_lanes": 4}, {"spec": True}])
+def test_overlapped_frames_bit_exact(variant, gpu_available):
     """RTC_F_OVERLAP (frame pipelining): launches that do not join their sky pass, with the next launch's
     preparation (tile cull into the other scratch half) overlapping it.  Eight frames over three cameras, each
     consumed (copied) once its frame event fires, and two frames of different cameras into one buffer: every
-    frame equals a joined rtc_render bit for bit."""
+    frame equals a joined rtc_render bit for bit (with each geometry-pixel kernel)."""
     import torch
 
     tris, _ = load_tris("ultracomplex")
@@ -349,7 +350,7 @@ def test_overlapped_frames_bit_exact(gpu_available):
             rt.camera_basis((-5.3, -1.2, -4.1), (1.2, -1.4, 0.7), 0.9)]
     W, H, spp = 256, 144, 8
     ref = [rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))[0] for c in cams]
-    cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True)
+    cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True, **variant)
     ds = rt.DeviceScene(tris, None)
     st, cp = torch.cuda.Stream(), torch.cuda.Stream()
     bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
