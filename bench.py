@@ -473,6 +473,23 @@ def main():
                     traffic = pm["hbm_bytes_per_launch"]
             except Exception:
                 traffic = None
+        # VALU issue of the dominant kernel (profiles/r02_e_pmc_breakdown.json: rocprofv3 SQ counters of one launch of
+        # this workload): wave-level VALU instructions x 2 cycles (FP64 x 4) over what 1024 SIMDs (256 CUs x 4)
+        # issue at 2.4 GHz in the measured kernel time -- how close the kernel runs to its own issue bound
+        issue = None
+        brk = os.path.join(REPO, "profiles", "r02_e_pmc_breakdown.json")
+        if os.path.exists(brk) and args.workload == "ultracomplex_1080p64" and world == 1:
+            try:
+                pd = json.load(open(brk))["rtc_render_chain"]["_per_dispatch"]
+                f64 = pd["SQ_INSTS_VALU_ADD_F64"] + pd["SQ_INSTS_VALU_MUL_F64"] + pd["SQ_INSTS_VALU_FMA_F64"] + \
+                    pd["SQ_INSTS_VALU_TRANS_F64"]
+                cyc = 2.0 * pd["SQ_INSTS_VALU"] + 2.0 * f64
+                issue = {"valu_insts_per_launch": int(pd["SQ_INSTS_VALU"]), "fp64_insts_per_launch": int(f64),
+                         "salu_insts_per_launch": int(pd["SQ_INSTS_SALU"]),
+                         "valu_issue_frac": round(cyc / (1024 * dom_ms * 1e-3 * 2.4e9), 4),
+                         "source": "profiles/r02_e_pmc_breakdown.json"}
+            except Exception:
+                issue = None
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -507,6 +524,7 @@ def main():
                          "hbm_achieved_gbs": (round(traffic / (dom_ms * 1e-3) / 1e9, 3) if traffic else None),
                          "hbm_peak_gbs": HBM_PEAK_GBS,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
+                         "issue": issue,
                          "note": "achieved: the ray-triangle tests the kernel evaluated x 57 flop / its device time "
                                  "(HIP events around it on the launch stream); traffic: rocprofv3 FETCH_SIZE x 2 + "
                                  "WRITE_SIZE per launch (profiles/pmc_traffic.json); hbm_achieved_gbs: traffic / "
