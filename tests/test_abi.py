@@ -67,3 +67,19 @@ def test_bad_arguments_rejected():
     assert L.rtc_deinterleave_async(None, 0, 0, 0, 0, None, None) == _abi.RTC_EINVAL
     assert L.rtc_write_bmp(b"/nonexistent/dir/x.bmp", 1, 1, None) == _abi.RTC_EINVAL
     assert b"rtc_" in L.rtc_last_error() or len(L.rtc_last_error()) > 0
+
+
+def test_flag_constants_match_header():
+    """Every RTC_F_* / RTC_E* / RTC_SEGMENT_COUNTERS value in include/rtc.h equals the ctypes mirror's."""
+    import re
+
+    import raytracingc_amd._abi as abi
+
+    txt = open(os.path.join(REPO, "include", "rtc.h")).read()
+    found = dict(re.findall(r"#define\s+(RTC_(?:F_\w+|E\w+|OK|SEGMENT_COUNTERS))\s+\(?(-?(?:0x)?[0-9a-fA-F]+)\)?", txt))
+    assert "RTC_F_OVERLAP" in found and "RTC_F_CHAIN_INLINE" in found
+    for name, val in found.items():
+        if hasattr(abi, name):
+            assert getattr(abi, name) == int(val, 0), name
+    for name in [n for n in found if n.startswith("RTC_F_")]:
+        assert hasattr(abi, name), f"{name} missing from raytracingc_amd/_abi.py"

@@ -388,6 +388,37 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
     ds.close()
 
 
+def test_overlap_with_counters_and_mixed_launches(gpu_available):
+    """An RTC_F_OVERLAP launch that asks for segment counters joins (the counts equal a joined launch's), and
+    joined / overlapped / no-tile-cull launches interleaved on one scene (the scratch halves and pending sky
+    passes) each produce their frame bit for bit."""
+    import torch
+
+    tris, _ = load_tris("complex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, spp = 200, 120, 6
+    ref, _, st = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))
+    ds = rt.DeviceScene(tris, None)
+    s = torch.cuda.current_stream()
+    seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device="cuda")
+    out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, spp, 10, True, overlap=True), out.data_ptr(), None,
+                         seg.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert int(seg[0]) == st["segments"] and int(seg[2]) == st["tri_tests"]
+    cfgs = [rt.RenderConfig(W, H, spp, 10, True, overlap=True), rt.RenderConfig(W, H, spp, 10, True),
+            rt.RenderConfig(W, H, spp, 10, True, overlap=True), rt.RenderConfig(W, H, spp, 10, True, overlap=True),
+            rt.RenderConfig(W, H, spp, 10, True, tile_cull=False), rt.RenderConfig(W, H, spp, 10, True, overlap=True)]
+    outs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in cfgs]
+    for c, o in zip(cfgs, outs):
+        ds.render_rows_async(scene, cam, c, o.data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()  # (the whole device: the unjoined sky passes too)
+    for k, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy(), ref), f"launch {k}"
+    ds.close()
+
+
 @pytest.mark.parametrize("variant", [{}, {"coop_lanes": 4}, {"coop_lanes": 8}, {"spec": True}, {"hoist": True},
                                      {"pipe": True}, {"chain_inline": True}, {"hoist": True, "chain_inline": True}])
 def test_spp_not_multiple_of_64(variant, gpu_available):
