@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """One rank's share of a frame at N GPUs (rows y = r + kN), rendered on one GPU: the per-rank device time that
 bounds strong scaling (the gather of the uint8 parts and the re-interleave come on top).  Not part of the product.
-Usage: scale_probe.py [frames] [W H spp] [kernel: chain|pipe|coop4]"""
+Usage: scale_probe.py [frames] [W H spp] [kernel: chain|pipe|coop4|overlap]  (overlap: the chain kernel with frame
+pipelining, RTC_F_OVERLAP -- the per-frame period of back-to-back frames instead of one frame's latency)"""
 import json
 import os
 import sys
@@ -17,7 +18,7 @@ from conftest import load_tris  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 kernel = sys.argv[5] if len(sys.argv) > 5 else "chain"
-extra = {"chain": {}, "pipe": {"pipe": True}, "coop4": {"coop_lanes": 4}}[kernel]
+extra = {"chain": {}, "pipe": {"pipe": True}, "coop4": {"coop_lanes": 4}, "overlap": {"overlap": True}}[kernel]
 tris, _ = load_tris("ultracomplex")
 scene, cam = rt.default_scene(), rt.camera_basis()
 ds = rt.DeviceScene(tris, None)
@@ -34,13 +35,25 @@ for n in (1, 2, 4, 8):
     for r in range(n):  # every rank's share: the slowest sets the frame
         cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, **extra)
         times = []
-        for _ in range(frames):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, None, stream.cuda_stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1))
+        if kernel == "overlap":  # the period of 20 back-to-back pipelined frames (device synchronised around them)
+            for _ in range(frames):
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(20):
+                    ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, None, stream.cuda_stream)
+                torch.cuda.synchronize()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1) / 20)
+        else:
+            for _ in range(frames):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                ds.render_rows_async(scene, cam, cfg, out.data_ptr(), None, None, stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1))
         ms = sorted(times)[len(times) // 2]
         per.append(round(ms, 4))
         worst = max(worst, ms)
