@@ -17,7 +17,8 @@ cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True),
        "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
        "empty": rt.RenderConfig(1920, 1080, 64, 10, True),
        "share8": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8),
-       "share8c4": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8, coop_lanes=4)}[v]
+       "share8c4": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8, coop_lanes=4),
+       "ns4k": rt.RenderConfig(3840, 2160, 64, 10, True)}[v]
 if v == "empty":
     tris = tris[:0]
 for _ in range(reps):
