@@ -3,18 +3,20 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ultracomplex_1080p64|...]
 
-A step = one frame, timed as SURVEY.md §8(d) / BASELINE.md §3 define it: from the render launch until the
-frame's Color[W*H] is in host memory (the buffer main.c:305 hands to stbi_write_bmp).  Every rank renders its
-interleaved rows (y = rank + k*N, main.c:84 lifted to GPUs) with the HIP kernels, the uint8 parts are gathered
-to rank 0 over RCCL (torch.distributed `nccl`) and re-interleaved there, and rank 0 copies the frame into pinned
-host memory (hipMemcpyAsync on a copy stream; frame k's copy overlaps frame k+1's render, double-buffered).
-The scene (the reference loader's Triangle[], tests/golden/scenes) is resident in HBM before timing.
+A step = one frame, timed as SURVEY.md §8(d) / BASELINE.md §3 define it: from the render launch until the frame's
+Color[W*H] is in host memory (the buffer main.c:305 hands to stbi_write_bmp).  Rank r of N renders the interleaved
+rows y = r + k*N (main.c:84 lifted to GPUs) with the HIP kernels and copies them with its own SDMA engines straight
+into their places of the shared host frame (rtc_frame_loop: native pipelined frames, rtc_copy_rows_d2h_dma; a POSIX
+shared-memory frame every rank maps at N > 1) -- the reference's threads likewise write their rows into one image
+(main.c:285-302).  At N > 1 the RCCL path is measured beside it: the parts gathered to rank 0's GPU over xGMI
+(torch.distributed `nccl` = RCCL) and re-interleaved there (the device-resident frame).  The scene (the reference
+loader's Triangle[], tests/golden/scenes) is resident in HBM before timing.
 
 Prints ONE JSON line on rank 0.  `value` = W*H*spp*K / t / 1e6 over the whole job (strong scaling: the frame is
-fixed, N GPUs split it).  `roofline` is the dominant (heavy-tile) kernel against the FP32 VALU peak with the
-survey's algorithmic 57 flop per ray-triangle test (SURVEY.md §8 d); `cpu_baseline` is the CPU restatement of
-the reference (oracle/, "port") on the same workload on the box's host cores, beside the reference itself
-compiled here (oracle/_ref/rtc_ref), rank 0 at N = 1 only.
+fixed, N GPUs split it).  `roofline` covers the split launch's kernels (rtc_render_chain, rtc_render_sky) with the
+live HIP-event times and the committed rocprofv3 PMC digest of the same workload (profiles/); `cpu_baseline` is the
+CPU restatement of the reference (oracle/, "port") on the box's host cores beside the reference itself compiled here
+(oracle/_ref/rtc_ref), rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -91,10 +93,11 @@ def cpu_info() -> dict:
 
 def cpu_baseline(tris, tonly, scene, cam, W, H, spp, budget_samples, gpu_colors, gpu_accum):
     """The reference algorithm on the host: the CPU restatement (oracle/rtc_oracle.c, bit-identical to the
-    reference on every golden fixture; gcc -O3, no FMA) with row-interleaved pthreads like main.c:84 at
-    threads = nproc and at the reference's 12, plus the reference's own sources compiled here
-    (oracle/_ref/rtc_ref, 12 threads, its own main) when the whole frame fits the budget.  Rows
-    y = 0, s, 2s, ... of the same frame with s = ceil(samples / budget) (s = 1 at the metric's config)."""
+    reference on every golden fixture; gcc -O3, no FMA) with row-interleaved pthreads like main.c:84, at the
+    threads this process may actually run (min(nproc, affinity, cgroup quota)), at nproc and at the reference's 12;
+    `value` is the fastest of them.  The reference's own sources compiled here (oracle/_ref/rtc_ref, 12 threads,
+    its own main) are timed beside it when the whole frame fits the budget.  Rows y = 0, s, 2s, ... of the same
+    frame with s = ceil(samples / budget) (s = 1 at the metric's config)."""
     import hashlib
 
     import numpy as np
@@ -113,20 +116,32 @@ def cpu_baseline(tris, tonly, scene, cam, W, H, spp, budget_samples, gpu_colors,
         return time.perf_counter() - t0, colors, accum, seg
 
     n_all = info["nproc"]
-    dt, ccol, cacc, seg = run(n_all)
-    dt12, _, _, _ = run(REF_THREADS)
+    quota = info.get("cgroup_cpus")
+    usable = min(n_all, info.get("affinity", n_all), int(quota) if quota else n_all)
+    counts = sorted({max(1, usable), n_all, REF_THREADS})
+    runs = {}
+    ccol = cacc = seg = None
+    for n in counts:
+        dt, col, acc, sg = run(n)
+        runs[n] = dt
+        if ccol is None:
+            ccol, cacc, seg = col, acc, sg
     rows = ccol.shape[0]
     samples = rows * W * spp
+    best = min(runs, key=runs.get)
     res = {
-        "value": samples / dt / 1e6, "unit": "Mrays/s", "cores": n_all, "kind": "port",
-        "threads": n_all, "value_12t": round(samples / dt12 / 1e6, 3),
+        "value": round(samples / runs[best] / 1e6, 3), "unit": "Mrays/s", "cores": best, "kind": "port",
+        "threads": best,
+        "by_threads": {str(n): round(samples / t / 1e6, 3) for n, t in sorted(runs.items())},
+        "usable_cpus": usable,
         "cpu_model": info.get("model"),
         "topology": f"{info.get('sockets')} sockets x {info.get('cores_per_socket')} cores x "
                     f"{info.get('threads_per_core')} SMT = nproc {info['nproc']}; affinity {info['affinity']} CPUs, "
                     f"cgroup quota {info.get('cgroup_cpus')} CPUs",
         "sample": (f"{'the whole frame' if stride == 1 else f'rows y = 0 mod {stride} of the frame'} ({rows} rows x "
-                   f"{W} x {spp} spp = {samples} samples, {seg} segments), render loop only: {dt:.2f} s on {n_all} "
-                   f"threads, {dt12:.2f} s on {REF_THREADS}; oracle/rtc_oracle.c (gcc -O3, no FMA)"),
+                   f"{W} x {spp} spp = {samples} samples, {seg} segments), render loop only, timed at "
+                   + ", ".join(f"{n} threads {runs[n]:.2f} s" for n in counts)
+                   + "; value = the fastest; oracle/rtc_oracle.c (gcc -O3, no FMA)"),
     }
     g_rows = gpu_colors[::stride]
     res["u8_mismatch_vs_gpu"] = int((g_rows != ccol).any(-1).sum())
@@ -159,7 +174,95 @@ def cpu_baseline(tris, tonly, scene, cam, W, H, spp, budget_samples, gpu_colors,
     return res
 
 
+# ---- roofline inputs committed under profiles/ ------------------------------------------------------------
+def pmc_digest(workload, world):
+    """profiles/pmc_<workload>.json (tools/pmc_digest.py over this workload's rocprofv3 runs): per kernel the
+    rocprof average duration and per-dispatch counters -- VALU/SALU/LDS instructions, FP64 mix, LDS bank conflicts,
+    FETCH_SIZE / WRITE_SIZE -- and which kernel the kernel trace names dominant."""
+    path = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        dg = json.load(open(path))
+    except Exception:
+        return None
+    return dg if dg.get("n_gpus", 1) == world else None
+
+
+def kernel_roofline(name, live_ms, dg, work):
+    """One kernel's roofline entry.  bound "valu": the path has no dense contraction (no MFMA) and its compulsory
+    HBM traffic is tiny, so each kernel is held to its own VALU issue: wave-level VALU instructions x 2 cycles
+    (FP64 x 4) over what 1024 SIMDs issue at 2.4 GHz in the measured time (valu_issue_frac); achieved / peak is the
+    survey's algorithmic work (SURVEY.md §8 d: 57 flop per ray-triangle test) where the kernel does that work."""
+    e = {"ms": round(live_ms, 4) if live_ms else None}
+    k = (dg or {}).get("kernels", {}).get(name)
+    if k:
+        pd = k["per_dispatch"]
+        valu = pd.get("SQ_INSTS_VALU")
+        f64 = sum(pd.get(c, 0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        ms = live_ms or k.get("rocprof_avg_ms")
+        if valu and ms:
+            e["valu_insts_per_launch"] = int(valu)
+            e["fp64_insts_per_launch"] = int(f64)
+            e["valu_issue_frac"] = round((2.0 * valu + 2.0 * f64) / (1024 * ms * 1e-3 * 2.4e9), 4)
+        for c, key in (("SQ_INSTS_SALU", "salu_insts_per_launch"), ("SQ_INSTS_LDS", "lds_insts_per_launch"),
+                       ("SQ_LDS_BANK_CONFLICT", "lds_bank_conflict_cycles_per_launch")):
+            if c in pd:
+                e[key] = int(pd[c])
+        if "traffic_bytes" in k:
+            e["traffic"] = k["traffic_bytes"]
+            e["traffic_note"] = k.get("traffic_note")
+            if ms:
+                e["hbm_gbs"] = round(k["traffic_bytes"] / (ms * 1e-3) / 1e9, 2)
+        e["rocprof_avg_ms"] = k.get("rocprof_avg_ms")
+        e["source"] = dg.get("source")
+    if work:
+        e.update(work)
+    return e
+
+
 # ---- GPU ---------------------------------------------------------------------------------------------
+class SharedFrames:
+    """nbuf host frames [H, W, 3] every rank of the node maps (POSIX shared memory, created by local rank 0),
+    page-locked in each process (rtc_host_register) so the SDMA engines write into them."""
+
+    def __init__(self, name, nbuf, H, W, local, barrier):
+        import mmap
+
+        import numpy as np
+
+        import raytracingc_amd as rt
+
+        self.path = f"/dev/shm/{name}"
+        self.nbytes = nbuf * H * W * 3
+        if local == 0:
+            fd = os.open(self.path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, self.nbytes)
+            os.close(fd)
+        barrier()
+        fd = os.open(self.path, os.O_RDWR)
+        self.mm = mmap.mmap(fd, self.nbytes)
+        os.close(fd)
+        self.arr = np.frombuffer(self.mm, np.uint8).reshape(nbuf, H, W, 3)
+        self.arr.reshape(-1)[::4096] = 0  # fault the pages in before registering
+        rt.host_register(self.arr.ctypes.data, self.nbytes)
+        self.local = local
+
+    def ptr(self, b):
+        return self.arr[b].ctypes.data
+
+    def close(self, barrier):
+        import raytracingc_amd as rt
+
+        rt.host_unregister(self.arr.ctypes.data)
+        del self.arr
+        self.mm.close()
+        barrier()
+        if self.local == 0 and os.path.exists(self.path):
+            os.unlink(self.path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,14 +272,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
                     help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
-    ap.add_argument("--d2h", default="dma", choices=["dma", "kernel", "runtime"],
-                    help="how Color[] reaches host memory: the SDMA engines (rtc_copy_d2h_dma), a 32-workgroup copy "
-                         "kernel (rtc_copy_async) or hipMemcpyAsync")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="join every frame's sky pass into the render stream (no frame pipelining)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
-    ap.add_argument("--force-gather", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--diag-repeat", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="N > 1: process group backend (auto: nccl = RCCL when every rank has its own GPU; gloo lets "
+                         "ranks share one GPU for a rehearsal, without the RCCL leg)")
     args = ap.parse_args()
 
     import numpy as np
@@ -191,305 +290,179 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    # --force-gather: the multi-GPU data path (per-rank parts, RCCL gather on its own stream, re-interleave) with a
-    # single rank -- its streams, events and RCCL calls exercised on a one-GPU box (RCCL refuses two ranks on one
-    # device, so N > 1 itself cannot be rehearsed there)
-    multi = world > 1 or args.force_gather
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    multi = world > 1
+    backend = None
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        backend = args.backend if args.backend != "auto" else ("nccl" if ndev >= world else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if multi:
+            dist.barrier()
+
+    def allreduce_max(v):
+        if not multi:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def allreduce_sum(vals):
+        if not multi:
+            return vals
+        t = torch.tensor(vals, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        return [int(v) for v in t.tolist()]
 
     scene_name, W, H, spp = WORKLOADS[args.workload]
     tris, tonly = load_scene(scene_name)
     scene = rt.default_scene()
     cam = rt.camera_basis()
-    ds = rt.DeviceScene(tris, None, device=local)
+    ds = rt.DeviceScene(tris, None, device=gpu)
     seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device=dev)
     rows = rows_per_rank(H, world)
-    # the frames render on a non-blocking stream of their own (not the legacy default stream, whose implicit
-    # synchronisation with other streams costs the overlapped D2H); the copies on a second one
     stream = torch.cuda.Stream(dev)
-    copy_stream = torch.cuda.Stream(dev)
-    gather_stream = torch.cuda.Stream(dev)  # N > 1: RCCL gather + re-interleave of each frame, after its render
-    # three frame buffers: frame k+2 renders while frame k's D2H (issued at frame k+1's geometry-done event) may
-    # still be in flight, so the copy is off the render's critical path
     nbuf = 3
-    parts = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if multi else None
-    gathered = ([torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-                if (multi and rank == 0) else None)
-    part_free = [None] * nbuf  # N > 1: parts[b]'s previous gather has finished
-    frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
-    host = [torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)] if rank == 0 else None
+    # this rank's compact rows of each frame in HBM; the host frames: pinned (N = 1) or node-shared (N > 1)
+    dev_rows = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    shared = None
+    if multi:
+        shared = SharedFrames(f"rtc_bench_{os.environ.get('MASTER_PORT', '0')}", nbuf, H, W, local, barrier)
+        host_ptr = [shared.ptr(b) + rank * W * 3 for b in range(nbuf)]
+        host_frame = lambda b: shared.arr[b]  # noqa: E731
+    else:
+        host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
+        host_ptr = [h.data_ptr() + rank * W * 3 for h in host]
+        host_frame = lambda b: host[b].numpy()  # noqa: E731
+    pitch = world * W * 3
 
-    # the library records geo_ev on the render stream once a frame's geometry-pixel kernels are enqueued
-    # (rtc_scene_set_geometry_event): the previous frame's D2H starts there, overlapping this frame's sky pass
-    # rather than the start of its persistent geometry kernel (a blit kernel holding CU slots then would delay
-    # some of that kernel's workgroups for the whole copy)
-    geo_ev = torch.cuda.Event()
-    geo_ev.record(stream)
-    torch.cuda.synchronize(dev)
-    ds.set_geometry_event(geo_ev.cuda_event)
+    cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
+    cfg_r = rank_config(cfg_joined, rank, world)
 
-    def render_step(cfg, b, count=False):
-        """One frame into device frame buffer b (rank 0: rendered, or gathered and re-interleaved); returns the
-        event at which frame buffer b holds the whole frame.  The library records the frame event once both of
-        its passes are written (rtc_scene_set_frame_event: after the join, or with cfg.overlap -- frame
-        pipelining, the next frame's preparation overlapping this one's sky pass -- on its side stream); the
-        gather (RCCL, N > 1) and the D2H wait for it.  count: the kernels also add into the segment counters
-        (instrumentation: a separate untimed frame)."""
-        cfg_r = rank_config(cfg, rank, world)
-        segp = seg.data_ptr() if count else None
-        ready = torch.cuda.Event()
-        ready.record(stream)  # creates the hipEvent_t (a torch event has none before its first record)
-        # the library records the frame event while enqueuing the launch; it is cleared right after, so that no
-        # later launch records an event this function's caller may already have released
-        ds.set_frame_event(ready.cuda_event)
-        if not multi:
-            ds.render_rows_async(scene, cam, cfg_r, frames[b].data_ptr(), None, segp, stream.cuda_stream)
-            ds.set_frame_event(None)
-            return ready
-        if part_free[b] is not None:  # parts[b] is rewritten once its previous gather has read it
-            stream.wait_event(part_free[b])
-        ds.render_rows_async(scene, cam, cfg_r, parts[b].data_ptr(), None, segp, stream.cuda_stream)
-        ds.set_frame_event(None)
-        gather_stream.wait_event(ready)
-        with torch.cuda.stream(gather_stream):  # the gather (RCCL) orders itself after the frame on this stream
-            dist.gather(parts[b], gather_list=list(gathered[b].unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                rt.deinterleave_async(gathered[b].data_ptr(), world, rows, W, H, frames[b].data_ptr(),
-                                      gather_stream.cuda_stream)
-        done = torch.cuda.Event()
-        done.record(gather_stream)
-        part_free[b] = done
-        return done
+    def loop(cfg, frames):
+        return ds.frame_loop(scene, cam, cfg, [t.data_ptr() for t in dev_rows], host_ptr, pitch, frames,
+                             stream.cuda_stream)
 
-    nbytes = H * W * 3
-
-    def d2h_now(b, st):
-        """The D2H of frame buffer b into pinned host buffer b, ordered after the work enqueued on stream st so
-        far; returns when it is done (dma) or enqueued on st (kernel, runtime)."""
-        if args.d2h == "dma":
-            st.synchronize()
-            rt.copy_d2h_dma(host[b].data_ptr(), frames[b].data_ptr(), nbytes)
-        elif args.d2h == "kernel":
-            rt.copy_async(host[b].data_ptr(), frames[b].data_ptr(), nbytes, 32, st.cuda_stream)
-        else:
-            with torch.cuda.stream(st):
-                host[b].copy_(frames[b], non_blocking=True)
-
-    copy_ms = []  # dma: each frame copy's duration as the copying thread saw it (the last run)
-
-    def run(cfg, steps, warmup, d2h=True):
-        """warmup + steps frames; the timed region spans the steps frames, each rendered and (rank 0, d2h) copied
-        into pinned host memory, the copy of frame k overlapping the renders of the next frames:
-          dma     the SDMA engines (rtc_copy_d2h_dma) from a host thread that waits for frame k's event;
-          kernel  a 32-workgroup copy kernel (rtc_copy_async) on a copy stream, from frame k+1's geometry-done
-                  event (rtc_scene_set_geometry_event) so that it overlaps frame k+1's sky pass;
-          runtime hipMemcpyAsync (the runtime's blit kernel), likewise.
-        Frame buffer b is reused only once its previous copy has finished."""
-        use_d2h = d2h and rank == 0
-        copy_ms.clear()
-        if use_d2h and args.d2h == "dma":
-            jobs = queue.Queue()
-            free = [threading.Event() for _ in range(nbuf)]
-            for e in free:
-                e.set()
-            err = []
-
-            def worker():
-                while True:
-                    job = jobs.get()
-                    if job is None:
-                        return
-                    b, ev = job
-                    try:
-                        ev.synchronize()
-                        c0 = time.perf_counter()
-                        rt.copy_d2h_dma(host[b].data_ptr(), frames[b].data_ptr(), nbytes)
-                        copy_ms.append((time.perf_counter() - c0) * 1e3)
-                    except Exception as e:  # surfaced by the main thread
-                        err.append(e)
-                    free[b].set()
-
-            def frames_loop(n):
-                th = threading.Thread(target=worker, daemon=True)
-                th.start()
-                for k in range(n):
-                    b = k % nbuf
-                    free[b].wait()
-                    free[b].clear()
-                    jobs.put((b, render_step(cfg, b)))
-                jobs.put(None)
-                th.join()
-                if err:
-                    raise err[0]
-        else:
-            copied = [None] * nbuf
-
-            def copy_after(b, *after):
-                for e in after:
-                    copy_stream.wait_event(e)
-                d2h_now(b, copy_stream)
-                done = torch.cuda.Event()
-                done.record(copy_stream)
-                return done
-
-            def frames_loop(n):
-                pending = None
-                for k in range(n):
-                    b = k % nbuf
-                    if copied[b] is not None:  # frame buffer b is free once its previous D2H has finished
-                        stream.wait_event(copied[b])
-                        gather_stream.wait_event(copied[b])
-                    ready = render_step(cfg, b)
-                    if use_d2h:
-                        if pending is not None:
-                            copied[pending[0]] = copy_after(pending[0], pending[1], geo_ev)
-                        pending = (b, ready)
-                if use_d2h and pending is not None:
-                    copied[pending[0]] = copy_after(pending[0], pending[1])
-
-        frames_loop(warmup)
-        if multi:
-            dist.barrier()
+    def timed(cfg, steps, warmup):
+        """warmup + steps pipelined frames (rtc_frame_loop: render with RTC_F_OVERLAP, each frame's rows copied into
+        the host frame by the SDMA engines while the next frames render); the timed region spans the steps frames,
+        barrier + device synchronisation on both sides, max over ranks."""
+        if warmup:
+            loop(cfg, warmup)
+        barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        frames_loop(steps)
+        st = loop(cfg, steps)
         torch.cuda.synchronize(dev)
-        if multi:
-            dist.barrier()
-        dt = time.perf_counter() - t0
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        if multi:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        # the work counters of one more frame of the same configuration (untimed; every frame is identical)
-        seg.zero_()
-        render_step(cfg, 0, count=True)
-        torch.cuda.synchronize(dev)
-        segs = seg.clone()
-        if multi:
-            dist.all_reduce(segs)
-        return float(t[0]), [int(v) for v in segs.tolist()]
+        barrier()
+        dt = allreduce_max(time.perf_counter() - t0)
+        return dt, st
 
-    # the timed frames are pipelined (RenderConfig.overlap, RTC_F_OVERLAP: frame k+1's preparation overlaps frame
-    # k's sky pass; same frames) unless --no-overlap; the settle, kernel-timing and latency frames are joined
-    cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
-    cfg = rt.RenderConfig(W, H, spp, 10, bool(tonly), overlap=not args.no_overlap)
-    # untimed frames for ~0.3 s: the GPU clocks settle before the kernel timing, the warmup and the timed region
+    def counters(cfg):
+        """the work counters of one more frame of the same configuration (untimed; every frame is identical)"""
+        seg.zero_()
+        ds.render_rows_async(scene, cam, cfg, dev_rows[0].data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        return allreduce_sum([int(v) for v in seg.tolist()])
+
+    # untimed frames for ~0.3 s: the GPU clocks settle before the kernel timing and the timed region
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < 0.3:
-        for k in range(10):
-            ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world),
-                                 (parts[0] if multi else frames[0]).data_ptr(), None, None, stream.cuda_stream)
-            if rank == 0:  # the pinned buffers' first copies are slow (mapping): make them here, untimed
-                d2h_now(k % nbuf, stream)
-        torch.cuda.synchronize(dev)
-    # per-kernel device times of the split launch (HIP events the library records around the geometry-pixel
-    # kernel on this stream and around the sky kernel on the scene's side stream), averaged over frames rendered
-    # back to back at settled clocks, like rocprofv3's kernel trace of the same command
-    heavy_ms = sky_ms = None
+        loop(cfg_r, 10)
+    # per-kernel device times of the split launch (HIP events the library records around rtc_render_chain on the
+    # launch stream and around rtc_render_sky on the scene's side stream), averaged over joined frames rendered back
+    # to back at settled clocks, like rocprofv3's kernel trace of the same command
     kt = []
     ds.set_timing(True)
     for _ in range(20):
-        ds.render_rows_async(scene, cam, rank_config(cfg_joined, rank, world), (parts[0] if multi else frames[0]).data_ptr(),
-                             None, None, stream.cuda_stream)
+        ds.render_rows_async(scene, cam, cfg_r, dev_rows[0].data_ptr(), None, None, stream.cuda_stream)
         k = ds.kernel_times()
         if k:
             kt.append(k)
     ds.set_timing(False)
+    chain_ms = sky_ms = None
     if kt:
-        hk = torch.tensor([sum(a for a, _ in kt) / len(kt), sum(b for _, b in kt) / len(kt)], dtype=torch.float64,
-                          device=dev)
-        if multi:
-            dist.all_reduce(hk, op=dist.ReduceOp.MAX)
-        heavy_ms, sky_ms = float(hk[0]), float(hk[1])
-    if multi:
-        dist.barrier()
+        chain_ms = allreduce_max(sum(a for a, _ in kt) / len(kt))
+        sky_ms = allreduce_max(sum(b for _, b in kt) / len(kt))
+    barrier()
 
-    if args.diag_repeat:  # diagnosis only: the same timed run a few times before the reported one
-        print(json.dumps({"diag_repeat_ms": [round(run(cfg, args.steps, args.warmup)[0] / args.steps * 1e3, 4)
-                                             for _ in range(args.diag_repeat)]}), flush=True)
-    t, (seg_calls, seg_traced, tri_tests, cluster_tests, discarded_tests) = run(cfg, args.steps, args.warmup)
+    t, lst = timed(cfg_r, args.steps, args.warmup)
+    seg_calls, seg_traced, tri_tests, cluster_tests, discarded_tests = counters(cfg_r)
     samples = W * H * spp
     value = samples * args.steps / t / 1e6
-    # the last frame of the timed run as it landed in host memory
-    host_frame = host[(args.steps - 1) % nbuf].numpy().copy() if rank == 0 else None
-    # the D2H of one frame: dma -- the median copy of the timed run (SDMA, overlapping the next frames' renders);
-    # kernel / runtime -- ten copies on their own after it
-    d2h_ms = None
-    if rank == 0 and args.d2h == "dma" and copy_ms:
-        d2h_ms = sorted(copy_ms)[len(copy_ms) // 2]
-    elif rank == 0:
-        torch.cuda.synchronize(dev)
-        c0 = time.perf_counter()
-        for k in range(10):
-            d2h_now(k % nbuf, copy_stream)
-        copy_stream.synchronize()
-        d2h_ms = (time.perf_counter() - c0) / 10 * 1e3
+    # the last frame of the timed run as it landed in host memory (every rank's rows)
+    frame_host = host_frame((args.steps - 1) % nbuf).copy() if rank == 0 else None
+    barrier()
 
     extras = {}
+    if multi and backend == "nccl":
+        extras["rccl_device_frame"] = rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev,
+                                                        barrier, allreduce_max)
     if not args.no_extras:
-        # device-only frames (no D2H), the bit-exact hoisted mode and the brute-force primary segments
-        td, _ = run(cfg, args.steps, 1, d2h=False)
+        # device-only frames (left in HBM), the bit-exact hoisted mode, the brute-force primary segments
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        cfg_o = dataclasses_replace(cfg_r, overlap=True)
+        for k in range(args.steps):
+            ds.render_rows_async(scene, cam, cfg_o, dev_rows[k % nbuf].data_ptr(), None, None, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        td = allreduce_max(time.perf_counter() - t0)
         extras["device_only"] = {"ms_per_step": round(td / args.steps * 1e3, 4),
                                  "value": round(samples * args.steps / td / 1e6, 3)}
-        ref_frame = frames[0].clone() if rank == 0 else None
-        th, (_, ht, htests, _, _) = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), hoist=True, overlap=cfg.overlap), args.steps, 1)
+        th, _ = timed(dataclasses_replace(cfg_r, hoist=True), args.steps, 1)
+        _, ht, htests, _, _ = counters(dataclasses_replace(cfg_r, hoist=True))
         extras["hoisted"] = {"value": round(samples * args.steps / th / 1e6, 3),
                              "ms_per_step": round(th / args.steps * 1e3, 4), "segments_traced": ht,
                              "tri_tests": htests,
-                             "bit_exact_vs_faithful": bool(rank != 0 or torch.equal(frames[0], ref_frame))}
+                             "bit_exact_vs_faithful": bool(rank != 0 or np.array_equal(
+                                 host_frame((args.steps - 1) % nbuf), frame_host))}
         nb = max(2, args.steps // 4)
-        tb, (_, _, btests, _, _) = run(rt.RenderConfig(W, H, spp, 10, bool(tonly), tile_cull=False), nb, 1)
+        tb, _ = timed(dataclasses_replace(cfg_r, tile_cull=False), nb, 1)
+        _, _, btests, _, _ = counters(dataclasses_replace(cfg_r, tile_cull=False))
         extras["no_tile_cull"] = {"value": round(samples * nb / tb / 1e6, 3), "ms_per_step": round(tb / nb * 1e3, 4),
                                   "tri_tests": btests}
-        # single-frame latency: render .. Color[] on the host, nothing overlapped
-        if rank == 0 and world == 1:
+        # single-frame latency: render .. Color[] on the host, nothing overlapped (N = 1)
+        if world == 1:
             lat = []
             for _ in range(5):
                 torch.cuda.synchronize(dev)
                 l0 = time.perf_counter()
-                ds.render_rows_async(scene, cam, cfg_joined, frames[0].data_ptr(), None, None, stream.cuda_stream)
-                d2h_now(0, stream)
+                ds.render_rows_async(scene, cam, cfg_joined, dev_rows[0].data_ptr(), None, None, stream.cuda_stream)
                 stream.synchronize()
+                rt.copy_d2h_dma(host_ptr[0], dev_rows[0].data_ptr(), H * W * 3)
                 lat.append((time.perf_counter() - l0) * 1e3)
             extras["frame_latency_ms"] = round(sorted(lat)[len(lat) // 2], 4)
 
     if rank == 0:
         T = len(tris)
         tests_per_launch = tri_tests / world
-        dom_ms = heavy_ms if heavy_ms else t / args.steps * 1e3
-        achieved_tf = tests_per_launch * FLOPS_PER_TEST / (dom_ms * 1e-3) / 1e12
+        dg = pmc_digest(args.workload, world)
+        chain_work = None
+        if chain_ms:
+            ach = tests_per_launch * FLOPS_PER_TEST / (chain_ms * 1e-3) / 1e12
+            chain_work = {"achieved_tflops": round(ach, 3), "peak_tflops": FP32_VALU_PEAK_TFLOPS,
+                          "frac_57flop": round(ach / FP32_VALU_PEAK_TFLOPS, 4),
+                          "work_per_launch": f"{tests_per_launch:.4g} ray-triangle tests x {FLOPS_PER_TEST} flop"}
+        kernels = {"rtc_render_chain": kernel_roofline("rtc_render_chain", chain_ms, dg, chain_work),
+                   "rtc_render_sky": kernel_roofline("rtc_render_sky", sky_ms, dg, {
+                       "work_per_launch": "getEnvironmentLight (raytracing.c:151-160) once per sample of every pixel "
+                                          "whose primary ray misses: 2 glibc powf + 2 smoothstep (f64 tails)"})}
+        dominant = (dg or {}).get("dominant") or max(kernels, key=lambda k: kernels[k].get("ms") or 0)
+        dk = kernels[dominant]
+        # the line's top-level roofline: the dominant kernel against its VALU issue bound (no MFMA, no HBM bound)
+        frac = dk.get("valu_issue_frac")
         bf_tf = seg_traced / world * T * FLOPS_PER_TEST / (t / args.steps) / 1e12
-        traffic = None
-        pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            try:
-                pm = json.load(open(pmc_path)).get(args.workload)
-                if pm and pm.get("n_gpus", 1) == world:
-                    traffic = pm["hbm_bytes_per_launch"]
-            except Exception:
-                traffic = None
-        # VALU issue of the dominant kernel (profiles/r02_e_pmc_breakdown.json: rocprofv3 SQ counters of one launch of
-        # this workload): wave-level VALU instructions x 2 cycles (FP64 x 4) over what 1024 SIMDs (256 CUs x 4)
-        # issue at 2.4 GHz in the measured kernel time -- how close the kernel runs to its own issue bound
-        issue = None
-        brk = os.path.join(REPO, "profiles", "r02_e_pmc_breakdown.json")
-        if os.path.exists(brk) and args.workload == "ultracomplex_1080p64" and world == 1:
-            try:
-                pd = json.load(open(brk))["rtc_render_chain"]["_per_dispatch"]
-                f64 = pd["SQ_INSTS_VALU_ADD_F64"] + pd["SQ_INSTS_VALU_MUL_F64"] + pd["SQ_INSTS_VALU_FMA_F64"] + \
-                    pd["SQ_INSTS_VALU_TRANS_F64"]
-                cyc = 2.0 * pd["SQ_INSTS_VALU"] + 2.0 * f64
-                issue = {"valu_insts_per_launch": int(pd["SQ_INSTS_VALU"]), "fp64_insts_per_launch": int(f64),
-                         "salu_insts_per_launch": int(pd["SQ_INSTS_SALU"]),
-                         "valu_issue_frac": round(cyc / (1024 * dom_ms * 1e-3 * 2.4e9), 4),
-                         "source": "profiles/r02_e_pmc_breakdown.json"}
-            except Exception:
-                issue = None
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -505,38 +478,30 @@ def main():
             "data": f"reference scene {scene_name}.obj (Triangle[] from the reference loader, tests/golden/scenes), "
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
-                       "max_bounce": 10, "triangles": T, "parallelism": f"rows mod {world} + RCCL gather",
-                       "step": "render + gather + re-interleave + D2H of Color[W*H] into pinned host memory "
-                               "(triple-buffered: frame k's D2H overlaps the next frames' renders; d2h_method)"
-                               + ("; frames pipelined: frame k+1's primary records and tile cull overlap frame k's "
-                                  "sky pass (RTC_F_OVERLAP), its geometry kernel starts after it" if cfg.overlap else
-                                  "; frames joined (--no-overlap)"),
+                       "max_bounce": 10, "triangles": T,
+                       "parallelism": f"rows mod {world}; each rank SDMA-copies its rows into the shared host frame"
+                                      + (f"; RCCL gather measured beside it ({backend})" if multi else ""),
+                       "step": "render + D2H of Color[W*H] into pinned host memory (rtc_frame_loop: frames pipelined, "
+                               "frame k+1's preparation overlapping frame k's sky pass; frame k's SDMA copy overlapping "
+                               "the next frames' renders; triple-buffered)",
                        "mode": "faithful (every sample re-traces its primary ray and every miss evaluates the "
                                "environment)"},
-            "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VALU_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VALU_PEAK_TFLOPS, 4),
-                         "traffic": traffic,
-                         "kernel": "rtc_render_chain (geometry pixels of the split launch; state-indexed samples)",
-                         "kernel_ms": round(dom_ms, 4),
-                         "sky_kernel_ms": round(sky_ms, 4) if sky_ms else None,
-                         "work_per_launch": f"{tests_per_launch:.4g} ray-triangle tests x {FLOPS_PER_TEST} flop",
-                         "cluster_tests_per_launch": cluster_tests // world,
-                         "hbm_achieved_gbs": (round(traffic / (dom_ms * 1e-3) / 1e9, 3) if traffic else None),
-                         "hbm_peak_gbs": HBM_PEAK_GBS,
+            "roofline": {"bound": "valu", "dominant": dominant,
+                         "achieved": dk.get("valu_issue_frac"), "peak": 1.0, "unit": "VALU issue fraction",
+                         "frac": frac, "traffic": dk.get("traffic"),
+                         "kernels": kernels,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
-                         "issue": issue,
-                         "note": "achieved: the ray-triangle tests the kernel evaluated x 57 flop / its device time "
-                                 "(HIP events around it on the launch stream); traffic: rocprofv3 FETCH_SIZE x 2 + "
-                                 "WRITE_SIZE per launch (profiles/pmc_traffic.json); hbm_achieved_gbs: traffic / "
-                                 "kernel time; bruteforce_equiv: segments x T (the reference's brute-force work) per "
-                                 "frame time"},
+                         "note": "per kernel: ms = HIP events around it on its own stream (live); valu_issue_frac = "
+                                 "(2 x VALU + 2 x FP64 wave instructions) / (1024 SIMDs x 2.4 GHz x ms), counters from "
+                                 "the committed rocprofv3 PMC digest of this workload (roofline.kernels.*.source); "
+                                 "frac_57flop = ray-triangle tests x 57 flop / ms / 157.3 TFLOP/s (SURVEY §8 d); "
+                                 "traffic = counter HBM bytes per launch (traffic_note: which correction); "
+                                 "bruteforce_equiv = segments x T x 57 per frame time, not a roofline"},
             "frame_ms": round(t / args.steps * 1e3, 4),
-            "d2h_method": {"dma": "rtc_copy_d2h_dma (SDMA engines, host copy thread)",
-                           "kernel": "rtc_copy_async (32 workgroups, copy stream)",
-                           "runtime": "hipMemcpyAsync (runtime blit kernel, copy stream)"}[args.d2h],
-            "host_frame_equals_device_frame": bool(rank != 0 or torch.equal(torch.from_numpy(host_frame),
-                                                                             frames[(args.steps - 1) % nbuf].cpu())),
-            "d2h_ms": round(d2h_ms, 4) if d2h_ms is not None else None,
+            "frame_loop": {"enqueue_ms_per_frame": round(lst["enqueue_ms"] / max(1, lst["frames"]), 4),
+                           "copy_ms_median": round(lst["copy_ms_median"], 4), "copy_ms_max": round(lst["copy_ms_max"], 4),
+                           "d2h": "rtc_copy_rows_d2h_dma (SDMA engines, the CPU agent nearest the GPU), native copy "
+                                  "thread"},
             "segments_per_frame": seg_calls,
             "segments_traced_per_frame": seg_traced,
             "msegments_per_s": round(seg_traced * args.steps / t / 1e6, 2),
@@ -544,21 +509,84 @@ def main():
             "discarded_tri_tests_per_frame": discarded_tests,
             "gtests_per_s": round(tri_tests * args.steps / t / 1e9, 2),
         }
-        if multi:
-            # the gathered, re-interleaved frame as it landed on the host == one GPU rendering the whole frame
-            ref1, _, _ = rt.render(tris, None, scene, cam, cfg_joined, device=local)
-            line["frame_equals_1gpu_render"] = bool(np.array_equal(host_frame, ref1))
+        # the frame as it landed in host memory == one GPU rendering the whole frame through rtc_render
+        ref1, gacc, _ = rt.render(tris, None, scene, cam, cfg_joined, device=gpu, want_accum=(world == 1))
+        line["host_frame_equals_rtc_render"] = bool(np.array_equal(frame_host, ref1))
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
-            # the GPU's float frame for the bit comparison (one more render through the C ABI)
-            _, gacc, _ = rt.render(tris, None, scene, cam, cfg_joined, device=local, want_accum=True)
-            cb = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_budget_samples, host_frame, gacc)
+            cb = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_budget_samples, frame_host, gacc)
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(line), flush=True)
+    barrier()
     ds.close()
+    if shared is not None:
+        shared.close(barrier)
     if multi:
         dist.destroy_process_group()
+
+
+def dataclasses_replace(cfg, **kw):
+    import dataclasses
+
+    return dataclasses.replace(cfg, **kw)
+
+
+def rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev, barrier, allreduce_max):
+    """N > 1, every rank on its own GPU: the device-frame path -- each frame's parts gathered to rank 0's GPU over
+    xGMI (torch.distributed `nccl` = RCCL) and re-interleaved there (rtc_deinterleave_async), pipelined like the
+    host-frame loop (render on one stream, the gather on another after the frame event).  Returns its timing and
+    whether the gathered frame equals the single-GPU render."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import raytracingc_amd as rt
+
+    nbuf = 3
+    stream, gst = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    parts = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    gathered = [torch.zeros((world, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
+    frames = [torch.zeros((H, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)] if rank == 0 else None
+    free = [None] * nbuf
+    cfg_o = dataclasses_replace(cfg_r, overlap=True)
+
+    def step(k):
+        b = k % nbuf
+        if free[b] is not None:
+            stream.wait_event(free[b])
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        ds.set_frame_event(ready.cuda_event)
+        ds.render_rows_async(scene, cam, cfg_o, parts[b].data_ptr(), None, None, stream.cuda_stream)
+        gst.wait_event(ready)
+        with torch.cuda.stream(gst):
+            dist.gather(parts[b], gather_list=list(gathered[b].unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                rt.deinterleave_async(gathered[b].data_ptr(), world, rows, W, H, frames[b].data_ptr(), gst.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(gst)
+        free[b] = done
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    barrier()
+    t = allreduce_max(time.perf_counter() - t0)
+    out = {"ms_per_step": round(t / args.steps * 1e3, 4),
+           "value": round(W * H * cfg_r.spp * args.steps / t / 1e6, 3),
+           "what": "frame gathered into rank 0's HBM over RCCL (ncclGather via torch.distributed) and re-interleaved; "
+                   "no D2H"}
+    if rank == 0:
+        ref1, _, _ = rt.render(tris, None, scene, cam, dataclasses_replace(cfg_r, row_start=0, row_stride=1),
+                               device=dev.index)
+        out["frame_equals_1gpu_render"] = bool(np.array_equal(frames[(args.steps - 1) % nbuf].cpu().numpy(), ref1))
+    return out
 
 
 if __name__ == "__main__":

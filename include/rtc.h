@@ -61,26 +61,30 @@ typedef struct RtcRenderDesc {
                                     does) instead of the 8x8 tile's candidate list; same output bit for bit */
 #define RTC_F_NO_REORDER    0x8  /* dispatch workgroups in raster order instead of heaviest first (for A/B
                                     timing; the frame is identical) */
-#define RTC_F_NO_COOP       0x10 /* tiles that see geometry are rendered like the rest, one lane per pixel
-                                    (rtc_render_kernel), instead of by the split launch's heavy-tile kernel
+#define RTC_F_NO_COOP       0x10 /* pixels that see geometry are rendered like the rest, one lane per pixel
+                                    (rtc_render_kernel), instead of by the split launch's rtc_render_chain
                                     (A/B timing; the frame is identical) */
 #define RTC_F_NO_CLUSTER_CULL 0x20 /* bounce rays test every triangle instead of only the clusters their
                                       half-line may reach (A/B timing; identical frame) */
-/* The split launch's heavy-tile kernel is rtc_render_chain (state-indexed samples: lanes evaluate the samples
- * that start at consecutive RNG offsets, then the chain of the reference's samples is walked in order).  At
- * most one of the next four flags selects an older kernel instead, for A/B timing (identical frame); two of
- * them together are RTC_EINVAL. */
-#define RTC_F_COOP4         0x40 /* cooperative kernel, 4 lanes per pixel split each segment */
-#define RTC_F_COOP8         0x80 /* cooperative kernel, 8 lanes per pixel */
-#define RTC_F_PIPE          0x200 /* two samples in flight per pixel (faithful launches only: with
-                                     RTC_F_HOIST_PRIMARY it is RTC_EINVAL) */
-#define RTC_F_SPEC          0x100 /* sample-parallel speculation verified in sample order (lanes = samples) */
+/* The split launch renders the pixels that see geometry with rtc_render_chain (state-indexed samples: lanes
+ * evaluate the samples that start at consecutive RNG offsets, then the chain of the reference's samples is walked
+ * in order).  0x40, 0x80, 0x100 and 0x200 selected older kernels for A/B timing; they were removed and these flags
+ * are now RTC_EINVAL. */
+#define RTC_F_COOP4         0x40 /* removed: RTC_EINVAL */
+#define RTC_F_COOP8         0x80 /* removed: RTC_EINVAL */
+#define RTC_F_PIPE          0x200 /* removed: RTC_EINVAL */
+#define RTC_F_SPEC          0x100 /* removed: RTC_EINVAL */
 #define RTC_F_CHAIN_INLINE  0x400 /* rtc_render_chain adds each pixel's samples itself instead of deferring the
                                      in-order sum to a separate pass (A/B timing; identical frame) */
+#define RTC_F_HOST_ROWS     0x1000 /* rtc_render_multi only: no gather -- every device copies its rows straight into
+                                      their places of the host frame (rtc_copy_rows_d2h_dma, its own PCIe link);
+                                      without it the parts are gathered to device 0 over RCCL, re-interleaved there
+                                      and copied once.  Same frame bit for bit. */
 #define RTC_F_OVERLAP       0x800 /* frame pipelining (device-resident split only): the launch does not make
                                      `stream` wait for its sky pass, so the next launch on the same scene prepares
                                      its frame (primary records, tile cull; double-buffered scratch) while this
-                                     one's sky pass still runs; the next geometry-pixel kernel waits for it.  The
+                                     one's sky pass still runs; the next geometry-pixel kernel waits for it, and a
+                                     next launch that is not overlapped waits for it before its first kernel.  The
                                      frame is complete when the scene's frame event (rtc_scene_set_frame_event)
                                      fires; with segment counters requested the launch joins as usual.  Same
                                      frame bit for bit. */
@@ -173,15 +177,17 @@ int rtc_rows_selected(const RtcRenderDesc *d);
  * kernel (concurrent, on the scene's side stream); -1 when that launch recorded none.  Waits for that launch
  * to finish. */
 int rtc_scene_set_timing(RtcDeviceScene *s, int enable);
-/* Pipelining hook: every later launch on s records `event` (a caller-created hipEvent_t; NULL stops it) on the
- * launch's stream once the geometry-pixel kernels are enqueued, before the join with the sky pass; a caller can
- * start the previous frame's D2H there, so that the copy overlaps the sky pass instead of the next frame's
- * persistent geometry kernel (whose workgroups then all start at once). */
+/* Pipelining hooks.  Both are ONE-SHOT: the event is armed for the next launch on s that renders rows
+ * (rtc_render_rows_async with rows_selected > 0), which records it and forgets it, so no later launch can record
+ * an event its caller has released.  Arm again before every launch that should record one; NULL disarms.
+ * Geometry event: recorded on the launch's stream once the geometry-pixel kernels are enqueued, before the join
+ * with the sky pass; a caller can start the previous frame's D2H there, so that the copy overlaps the sky pass
+ * instead of the next frame's persistent geometry kernel (whose workgroups then all start at once). */
 int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event);
-/* Frame-completion hook: every later launch on s records `event` (NULL stops it) once the whole frame -- the
- * geometry pixels and the sky pass -- is written: on the launch's stream after the join, or with RTC_F_OVERLAP
- * (no join) on the scene's side stream after both passes.  Consumers of the frame (a D2H, a gather) wait for it.
- * The event must stay valid while launches record it (set NULL before destroying it). */
+/* Frame event: recorded once the whole frame -- the geometry pixels and the sky pass -- is written: on the launch's
+ * stream after the join, or with RTC_F_OVERLAP (no join) on the scene's side stream after both passes.  Consumers
+ * of the frame (a D2H, a gather) wait for it.  The event must stay valid until that launch has been enqueued
+ * (rtc_render_rows_async returned). */
 int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
@@ -196,6 +202,36 @@ int rtc_copy_async(void *dst, const void *src, size_t bytes, int blocks, void *s
  * frame's event first).  Unlike the runtime's D2H blit kernel it does not slow render kernels running at the
  * same time (~0.01 vs ~0.1 ms per 1080p frame). */
 int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes);
+/* Copy `rows` rows of `rowBytes` from device memory (row pitch srcPitch) into page-locked host memory (row pitch
+ * hostPitch) with the SDMA engines, blocking until done: one SDMA sub-window copy (all pointers, pitches and rowBytes
+ * multiples of 4), else one linear copy per row.  A rank's compact rows y = r + k*G (rtc_render_rows_async with
+ * rowStart r, rowStride G) land in their places of the interleaved host frame with hostDst = frame + r*W*3 and
+ * hostPitch = G*W*3 -- every GPU writes its own rows over its own PCIe link, as the reference's threads write their
+ * rows into the shared image (main.c:84, :285-302).  The host memory is hipHostMalloc'd or registered
+ * (rtc_host_register, e.g. a shared-memory frame all ranks map); the copy runs through the CPU agent nearest the
+ * source GPU. */
+int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void *devSrc, size_t srcPitch, size_t rowBytes,
+                          int rows);
+/* Page-lock (hipHostRegister, portable) / release an existing host range so the copies above can target it. */
+int rtc_host_register(void *p, size_t bytes);
+int rtc_host_unregister(void *p);
+
+/* Pipelined frames on one device, driven from native code (the per-frame host cost is the launch enqueue alone).
+ * Frame k renders d's rows with RTC_F_OVERLAP into devRows[k % nbuf] (device buffers of rows_selected*width*3 bytes)
+ * on `stream`; a copy thread waits for the frame's event and moves the rows into hostRows[k % nbuf] (page-locked,
+ * row pitch hostPitch) with rtc_copy_rows_d2h_dma; buffer b is rendered into again once its copy has finished.
+ * Returns when the last frame's rows are in host memory.  Uses the scene's frame event hook itself. */
+typedef struct RtcLoopStats {
+    double wallMs;       /* first enqueue .. the last frame's rows in host memory (host clock) */
+    int frames;
+    double enqueueMs;    /* host time spent in rtc_render_rows_async, summed over the frames */
+    double copyMsMedian; /* one frame's SDMA copy as the copy thread timed it: median and maximum */
+    double copyMsMax;
+} RtcLoopStats;
+int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d,
+                   void *const *devRows, void *const *hostRows, size_t hostPitch, int nbuf, int frames, void *stream,
+                   RtcLoopStats *stats);
+
 /* Re-assemble a row-interleaved gather: dCompact holds `parts` blocks of rowsPerPart*width*3 bytes, block
  * g holding rows y = g + k*parts; dOut receives the height*width*3 frame.  Asynchronous on `stream`. */
 int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,

@@ -26,14 +26,11 @@ from ._abi import (  # noqa: F401
     RAY_DT,
     RTC_F_DEBUG_BOUNCES,
     RTC_F_HOIST_PRIMARY,
-    RTC_F_COOP4,
-    RTC_F_COOP8,
     RTC_F_NO_CLUSTER_CULL,
     RTC_F_NO_COOP,
-    RTC_F_PIPE,
     RTC_F_CHAIN_INLINE,
     RTC_F_OVERLAP,
-    RTC_F_SPEC,
+    RTC_F_HOST_ROWS,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
     RTC_SEGMENT_COUNTERS,
@@ -45,6 +42,7 @@ from ._abi import (  # noqa: F401
     Ray,
     RtcCamera,
     RtcError,
+    RtcLoopStats,
     RtcRenderDesc,
     RtcStats,
     Scene,
@@ -138,13 +136,12 @@ class RenderConfig:
     debug_bounces: bool = False  # calcDebugColor (raytracing.c:242-260) instead of calcColor
     tile_cull: bool = True  # primary segments visit their 8x8 tile's candidate triangles (bit-exact)
     reorder: bool = True  # dispatch the workgroups that see geometry first (same frame)
-    coop: bool = True  # tiles that see geometry: 4 cooperating lanes per pixel (same frame)
+    coop: bool = True  # pixels that see geometry: the split launch's rtc_render_chain (same frame)
     cluster_cull: bool = True  # bounce rays skip triangle clusters they provably miss (same frame)
-    # heavy tiles: rtc_render_chain (state-indexed samples) unless one older kernel is chosen (same frame):
-    coop_lanes: int = 0  # 4 or 8: the cooperative kernel with that many lanes per pixel
-    spec: bool = False  # the sample-parallel speculative kernel
-    pipe: bool = False  # two samples in flight per pixel (faithful only)
     chain_inline: bool = False  # rtc_render_chain sums each pixel's samples itself (no deferred pass)
+    # render_multi: every device copies its rows straight into the host frame instead of the RCCL gather to
+    # device 0 (RTC_F_HOST_ROWS; same frame)
+    host_rows: bool = False
     # frame pipelining (DeviceScene.render_rows_async): the launch does not join its sky pass into the stream;
     # the frame is complete at the scene's frame event (DeviceScene.set_frame_event); same frame
     overlap: bool = False
@@ -153,9 +150,8 @@ class RenderConfig:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
-                | (RTC_F_COOP4 if self.coop_lanes == 4 else 0) | (RTC_F_COOP8 if self.coop_lanes == 8 else 0)
-                | (RTC_F_SPEC if self.spec else 0) | (RTC_F_PIPE if self.pipe else 0)
-                | (RTC_F_CHAIN_INLINE if self.chain_inline else 0) | (RTC_F_OVERLAP if self.overlap else 0))
+                | (RTC_F_CHAIN_INLINE if self.chain_inline else 0) | (RTC_F_OVERLAP if self.overlap else 0)
+                | (RTC_F_HOST_ROWS if self.host_rows else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
@@ -235,19 +231,38 @@ class DeviceScene:
         check(lib().rtc_scene_set_timing(self._h, int(enable)), "rtc_scene_set_timing")
 
     def set_geometry_event(self, event_handle: int | None):
-        """From now on every launch records this hipEvent_t (e.g. a torch.cuda.Event's cuda_event) on its stream
-        once the geometry-pixel kernels are enqueued, before the sky pass joins (rtc_scene_set_geometry_event);
-        None stops it."""
+        """Arm this hipEvent_t (e.g. a torch.cuda.Event's cuda_event) for the NEXT launch only: it records it on its
+        stream once the geometry-pixel kernels are enqueued, before the sky pass joins, and forgets it
+        (rtc_scene_set_geometry_event, one-shot); None disarms."""
         check(lib().rtc_scene_set_geometry_event(self._h, C.c_void_p(event_handle) if event_handle else None),
               "rtc_scene_set_geometry_event")
 
     def set_frame_event(self, event_handle: int | None):
-        """From now on every launch records this hipEvent_t once its whole frame is written: on its stream after
-        the join, or with RenderConfig.overlap on the scene's side stream (rtc_scene_set_frame_event); None
-        stops it.  The event must stay alive while launches record it: clear it (None) before releasing it.
-        (A torch.cuda.Event has no hipEvent_t before its first record: record it once first.)"""
+        """Arm this hipEvent_t for the NEXT launch only: it records it once its whole frame is written (on its stream
+        after the join, or with RenderConfig.overlap on the scene's side stream) and forgets it
+        (rtc_scene_set_frame_event, one-shot); None disarms.  A later launch never records it, so releasing the
+        event after that launch is safe.  (A torch.cuda.Event has no hipEvent_t before its first record: record
+        it once first.)"""
         check(lib().rtc_scene_set_frame_event(self._h, C.c_void_p(event_handle) if event_handle else None),
               "rtc_scene_set_frame_event")
+
+    def frame_loop(self, scene: Scene, cam: RtcCamera, cfg: RenderConfig, dev_rows: list, host_rows: list,
+                   host_pitch: int, frames: int, stream: int | None = None) -> dict:
+        """rtc_frame_loop: `frames` pipelined frames of cfg's rows, rendered into the device buffers dev_rows[k % n]
+        and copied (SDMA, native copy thread) into the page-locked host buffers host_rows[k % n] with row pitch
+        host_pitch; returns when the last frame is in host memory."""
+        n = len(dev_rows)
+        if len(host_rows) != n:
+            raise ValueError("frame_loop: one host buffer per device buffer")
+        d = cfg.desc()
+        dv = (C.c_void_p * n)(*dev_rows)
+        hv = (C.c_void_p * n)(*host_rows)
+        st = RtcLoopStats()
+        check(lib().rtc_frame_loop(self._h, C.byref(scene), C.byref(cam), C.byref(d), dv, hv, C.c_size_t(host_pitch),
+                                   n, int(frames), C.c_void_p(stream) if stream else None, C.byref(st)),
+              "rtc_frame_loop")
+        return {"wall_ms": st.wallMs, "frames": st.frames, "enqueue_ms": st.enqueueMs,
+                "copy_ms_median": st.copyMsMedian, "copy_ms_max": st.copyMsMax}
 
     def kernel_times(self):
         """(heavy-tile kernel ms, sky kernel ms) of the last split launch (None if it was not one)."""
@@ -276,6 +291,22 @@ def copy_async(dst_ptr: int, src_ptr: int, nbytes: int, blocks: int = 32, stream
 def copy_d2h_dma(host_ptr: int, dev_ptr: int, nbytes: int) -> None:
     """rtc_copy_d2h_dma: device -> page-locked host memory on the SDMA engines, blocking (GIL released)."""
     check(lib().rtc_copy_d2h_dma(C.c_void_p(host_ptr), C.c_void_p(dev_ptr), C.c_size_t(nbytes)), "rtc_copy_d2h_dma")
+
+
+def copy_rows_d2h_dma(host_ptr: int, host_pitch: int, dev_ptr: int, src_pitch: int, row_bytes: int, rows: int) -> None:
+    """rtc_copy_rows_d2h_dma: rows of device memory into page-locked host memory with a row pitch (SDMA, blocking):
+    a rank's interleaved rows straight into their places of the host frame."""
+    check(lib().rtc_copy_rows_d2h_dma(C.c_void_p(host_ptr), C.c_size_t(host_pitch), C.c_void_p(dev_ptr),
+                                      C.c_size_t(src_pitch), C.c_size_t(row_bytes), int(rows)), "rtc_copy_rows_d2h_dma")
+
+
+def host_register(ptr: int, nbytes: int) -> None:
+    """rtc_host_register: page-lock an existing host range (e.g. a shared-memory frame every rank maps)."""
+    check(lib().rtc_host_register(C.c_void_p(ptr), C.c_size_t(nbytes)), "rtc_host_register")
+
+
+def host_unregister(ptr: int) -> None:
+    check(lib().rtc_host_unregister(C.c_void_p(ptr)), "rtc_host_unregister")
 
 
 def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,

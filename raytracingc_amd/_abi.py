@@ -77,18 +77,29 @@ class RtcStats(C.Structure):
     ]
 
 
+class RtcLoopStats(C.Structure):
+    _fields_ = [
+        ("wallMs", C.c_double),
+        ("frames", C.c_int),
+        ("enqueueMs", C.c_double),
+        ("copyMsMedian", C.c_double),
+        ("copyMsMax", C.c_double),
+    ]
+
+
 RTC_F_HOIST_PRIMARY = 0x1
 RTC_F_DEBUG_BOUNCES = 0x2
 RTC_F_NO_TILE_CULL = 0x4
 RTC_F_NO_REORDER = 0x8
 RTC_F_NO_COOP = 0x10
 RTC_F_NO_CLUSTER_CULL = 0x20
-RTC_F_COOP4 = 0x40
+RTC_F_COOP4 = 0x40  # removed kernels: RTC_EINVAL
 RTC_F_COOP8 = 0x80
 RTC_F_SPEC = 0x100
 RTC_F_PIPE = 0x200
 RTC_F_CHAIN_INLINE = 0x400
 RTC_F_OVERLAP = 0x800
+RTC_F_HOST_ROWS = 0x1000
 RTC_SEGMENT_COUNTERS = 5  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
 
@@ -124,7 +135,8 @@ EXPORTS = [
     "rtc_render", "rtc_render_multi",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
-    "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma",
+    "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
+    "rtc_host_unregister", "rtc_frame_loop",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
 ]
@@ -179,6 +191,11 @@ def lib() -> C.CDLL:
     L.rtc_scene_set_frame_event.argtypes = [vp, vp]
     L.rtc_copy_async.argtypes = [vp, vp, sz, C.c_int, vp]
     L.rtc_copy_d2h_dma.argtypes = [vp, vp, sz]
+    L.rtc_copy_rows_d2h_dma.argtypes = [vp, sz, vp, sz, sz, ip]
+    L.rtc_host_register.argtypes = [vp, sz]
+    L.rtc_host_unregister.argtypes = [vp]
+    L.rtc_frame_loop.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp, sz, ip,
+                                 ip, vp, C.POINTER(RtcLoopStats)]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]
     L.rtc_render_rows_async.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp,
                                         vp, vp]

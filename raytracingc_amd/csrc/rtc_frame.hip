@@ -19,8 +19,13 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtc.h"
@@ -201,6 +206,10 @@ extern "C" int rtc_render(const Triangle *tris, int triCount, const Sphere *sphe
     return 0;
 }
 
+int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                               const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int G,
+                               Color *outImage, float *outAccum, RtcStats *stats, std::chrono::steady_clock::time_point t0);
+
 extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                                 const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
                                 Color *outImage, float *outAccum, RtcStats *stats)
@@ -214,6 +223,9 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         return rc;
     if (numDevices > n)
         return rtc_fail(RTC_EINVAL, "rtc_render_multi: %d devices requested, %d present", numDevices, n);
+    if (d->flags & RTC_F_HOST_ROWS)
+        return rtc_render_multi_host_rows(tris, triCount, spheres, sphereCount, scene, cam, d, numDevices, outImage,
+                                          outAccum, stats, t0);
     const Rccl &R = rccl();
     if (!R.ok)
         return rtc_fail(RTC_ENODEV, "rtc_render_multi: RCCL (librccl.so.1) could not be loaded: %s", dlerror());
@@ -239,6 +251,12 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         }
     } commGuard{R, comms};
 
+    /* device 0 also holds the gathered parts and the re-interleaved frame.  Declared before the parts (destroyed
+     * after them): the parts' guard synchronises every stream first, so no gather or copy still in flight on an
+     * error return touches freed memory. */
+    DevBuf<unsigned char> gathered, frame;
+    DevBuf<float> gatheredAcc, frameAcc;
+    PinnedBuf hColors;
     struct Part {
         RtcDeviceScene *s = nullptr;
         hipStream_t st = nullptr;
@@ -262,10 +280,6 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             }
         }
     } partsGuard{parts};
-    /* device 0 also holds the gathered parts, the re-interleaved frame and the events around the frame */
-    DevBuf<unsigned char> gathered, frame;
-    DevBuf<float> gatheredAcc, frameAcc;
-    PinnedBuf hColors;
     hipEvent_t eFrame = nullptr;
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
@@ -304,6 +318,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     }
 
     /* ---- the frame: render every part, gather to device 0 over RCCL, re-interleave, D2H ---- */
+    const auto f0 = std::chrono::steady_clock::now();
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
         RtcDeviceGuard dg(g);
@@ -334,15 +349,15 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
             return rc;
         HIP_TRY(hipMemcpyAsync(hColors.p, frame.p, (size_t)W * H * 3, hipMemcpyDeviceToHost, st0));
         HIP_TRY(hipEventRecord(eFrame, st0));
-        if (outAccum) /* a float row is 4x the bytes of a Color row: re-interleave it as 4W "pixels" */
-            if (int rc = rtc_deinterleave_async(gatheredAcc.p, G, rowsPer, 4 * W, H, frameAcc.p, st0))
-                return rc;
         HIP_TRY(hipEventSynchronize(eFrame));
     }
-    float frameMs = 0.f;
-    {
+    /* the frame time on the host clock: from before the first device's launch until Color[] is on the host (the
+     * devices' events cannot be compared across devices) */
+    const double frameMs = ms_since(f0);
+    if (outAccum) { /* a float row is 4x the bytes of a Color row: re-interleave it as 4W "pixels" */
         RtcDeviceGuard dg(0);
-        HIP_TRY(hipEventElapsedTime(&frameMs, parts[0].e0, eFrame));
+        if (int rc = rtc_deinterleave_async(gatheredAcc.p, G, rowsPer, 4 * W, H, frameAcc.p, parts[0].st))
+            return rc;
     }
     double renderMs = 0.0;
     unsigned long long seg[RTC_SEGMENT_COUNTERS] = {0};
@@ -367,12 +382,133 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     return 0;
 }
 
+/* RTC_F_HOST_ROWS: no gather -- each device copies its compact rows straight into their places of the pinned host
+ * frame (rtc_copy_rows_d2h_dma: host pitch G*W*3), over its own PCIe link, concurrently; the reference's threads
+ * likewise write their rows into the shared image (main.c:84, :285-302). */
+int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
+                               const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int G,
+                               Color *outImage, float *outAccum, RtcStats *stats, std::chrono::steady_clock::time_point t0)
+{
+    RtcDeviceGuard guard(-1);
+    const int W = d->width, H = d->height;
+    const int rowsPer = (H + G - 1) / G;
+    const size_t partPx = (size_t)rowsPer * (size_t)W;
+    PinnedBuf hColors, hAccum; /* before the parts: destroyed after their streams are synchronised */
+    HIP_TRY(hColors.alloc((size_t)W * H * 3));
+    if (outAccum)
+        HIP_TRY(hAccum.alloc((size_t)W * H * 3 * sizeof(float)));
+    struct Part {
+        RtcDeviceScene *s = nullptr;
+        hipStream_t st = nullptr;
+        DevBuf<unsigned char> col;
+        DevBuf<float> acc;
+        DevBuf<unsigned long long> seg;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        int rows = 0;
+        int rc = 0;
+        std::string err;
+    };
+    std::vector<Part> parts(G);
+    Events evs;
+    struct PartsGuard {
+        std::vector<Part> &p;
+        ~PartsGuard()
+        {
+            for (size_t g = 0; g < p.size(); ++g) {
+                RtcDeviceGuard dg((int)g);
+                if (p[g].st)
+                    (void)hipStreamSynchronize(p[g].st), (void)hipStreamDestroy(p[g].st);
+                rtc_scene_release(p[g].s);
+            }
+        }
+    } partsGuard{parts};
+    for (int g = 0; g < G; ++g) {
+        Part &p = parts[g];
+        RtcDeviceGuard dg(g);
+        RtcRenderDesc dg_desc = *d;
+        dg_desc.rowStart = g;
+        dg_desc.rowStride = G;
+        p.rows = rtc_rows_selected(&dg_desc);
+        if (int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s))
+            return rc;
+        HIP_TRY(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
+        HIP_TRY(p.col.alloc(partPx * 3 + 16, g));
+        if (outAccum)
+            HIP_TRY(p.acc.alloc(partPx * 3 * sizeof(float) + 16, g));
+        HIP_TRY(p.seg.alloc(kSegBytes, g));
+        HIP_TRY(hipMemset(p.seg.p, 0, kSegBytes));
+        HIP_TRY(evs.make(&p.e0));
+        HIP_TRY(evs.make(&p.e1));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    const auto f0 = std::chrono::steady_clock::now();
+    for (int g = 0; g < G; ++g) {
+        Part &p = parts[g];
+        RtcDeviceGuard dg(g);
+        RtcRenderDesc dg_desc = *d;
+        dg_desc.rowStart = g;
+        dg_desc.rowStride = G;
+        HIP_TRY(hipEventRecord(p.e0, p.st));
+        if (int rc = rtc_render_rows_async(p.s, scene, cam, &dg_desc, p.col.p, p.acc.p, p.seg.p, p.st))
+            return rc;
+        HIP_TRY(hipEventRecord(p.e1, p.st));
+    }
+    /* one host thread per device: wait for its rows, copy them into the frame (SDMA, own link) */
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g] {
+            Part &p = parts[g];
+            RtcDeviceGuard dg(g);
+            hipError_t e = hipEventSynchronize(p.e1);
+            if (e != hipSuccess) {
+                p.rc = rtc_fail(-(int)e, "rtc_render_multi: device %d: %s", g, hipGetErrorString(e));
+            } else {
+                p.rc = rtc_copy_rows_d2h_dma((unsigned char *)hColors.p + (size_t)g * W * 3, (size_t)G * W * 3,
+                                             p.col.p, (size_t)W * 3, (size_t)W * 3, p.rows);
+            }
+            if (p.rc)
+                p.err = rtc_last_error();
+        });
+    for (std::thread &t : th)
+        t.join();
+    const double frameMs = ms_since(f0);
+    for (int g = 0; g < G; ++g)
+        if (parts[g].rc)
+            return rtc_fail(parts[g].rc, "%s", parts[g].err.c_str());
+    double renderMs = 0.0;
+    unsigned long long seg[RTC_SEGMENT_COUNTERS] = {0};
+    for (int g = 0; g < G; ++g) {
+        Part &p = parts[g];
+        RtcDeviceGuard dg(g);
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.e0, p.e1));
+        renderMs = ms > renderMs ? ms : renderMs;
+        unsigned long long sg[RTC_SEGMENT_COUNTERS];
+        HIP_TRY(hipMemcpy(sg, p.seg.p, kSegBytes, hipMemcpyDeviceToHost));
+        for (int k = 0; k < RTC_SEGMENT_COUNTERS; ++k)
+            seg[k] += sg[k];
+        if (outAccum)
+            if (int rc = rtc_copy_rows_d2h_dma((float *)hAccum.p + (size_t)g * W * 3, (size_t)G * W * 3 * sizeof(float),
+                                               p.acc.p, (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float),
+                                               p.rows))
+                return rc;
+    }
+    memcpy(outImage, hColors.p, (size_t)W * H * 3);
+    if (outAccum)
+        memcpy(outAccum, hAccum.p, (size_t)W * H * 3 * sizeof(float));
+    fill_stats(stats, renderMs, frameMs, seg, d, (size_t)W * H, t0);
+    return 0;
+}
+
 /* ---- D2H through the copy engines ------------------------------------------------------------------------
  * The HIP runtime copies device memory into pinned host memory with a blit kernel (one workgroup per CU); while
- * render kernels run, those PCIe writes from the shader cores cost the render ~0.1 ms per 1080p frame, even
- * from a handful of workgroups (tools/copy_overlap_probe.py), whereas the SDMA engines' copy costs it ~0.01 ms
- * (tools/sdma_overlap_probe.py).  rtc_copy_d2h_dma drives the SDMA engines through the HSA runtime HIP itself
- * runs on: blocking, for a caller thread that pipelines frame copies behind the renders. */
+ * render kernels run, those PCIe writes from the shader cores cost the render ~0.1 ms per 1080p frame, even from a
+ * handful of workgroups, whereas the SDMA engines' copy costs it ~0.01 ms.  The copies below drive the SDMA engines
+ * through the HSA runtime HIP itself runs on, blocking, for a caller thread that pipelines frame copies behind the
+ * renders.  The destination is page-locked host memory: hipHostMalloc'd (HSA pointer type HSA) or registered
+ * (hipHostRegister / rtc_host_register: type LOCKED, reached by the GPU at its agent address).  The host side of the
+ * copy is the CPU agent nearest the source GPU (HSA_AMD_AGENT_INFO_NEAREST_CPU), so a GPU on the second socket does
+ * not stage through the first. */
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
@@ -402,6 +538,67 @@ DmaAgents &dma_agents()
     });
     return a;
 }
+
+/* one completion signal per calling thread, destroyed with the thread */
+struct DmaSignal {
+    hsa_signal_t s{0};
+    ~DmaSignal()
+    {
+        if (s.handle)
+            (void)hsa_signal_destroy(s);
+    }
+};
+
+/* wait until `sig` drops below 1; RTC_EIO when the copy reports an error (negative value) or has not completed
+ * after 20 s (a faulted or lost copy must not hang the caller) */
+int dma_wait(hsa_signal_t sig, const char *what)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 1000000,
+                                                                HSA_WAIT_STATE_BLOCKED);
+        if (v == 0)
+            return 0;
+        if (v < 0)
+            return rtc_fail(RTC_EIO, "%s: the copy engine reported an error (signal %lld)", what, (long long)v);
+        if (ms_since(t0) > 20000.0)
+            return rtc_fail(RTC_EIO, "%s: copy not completed after 20 s", what);
+    }
+}
+
+/* The source's GPU agent, the destination's GPU-visible address and the copy's CPU agent.  hostDst..+span must lie
+ * in one page-locked allocation. */
+int dma_endpoints(void *hostDst, size_t span, const void *devSrc, const char *what, hsa_agent_t &gpu, void *&dstAgent,
+                  hsa_agent_t &cpu)
+{
+    DmaAgents &a = dma_agents();
+    if (!a.ok)
+        return rtc_fail(RTC_ENODEV, "%s: no HSA CPU agent", what);
+    hsa_amd_pointer_info_t src{}, dst{};
+    src.size = sizeof(src);
+    dst.size = sizeof(dst);
+    if (hsa_amd_pointer_info(devSrc, &src, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        src.type != HSA_EXT_POINTER_TYPE_HSA)
+        return rtc_fail(RTC_EINVAL, "%s: source is not device memory", what);
+    if (hsa_amd_pointer_info(hostDst, &dst, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS)
+        return rtc_fail(RTC_EINVAL, "%s: destination is not page-locked host memory", what);
+    const size_t off = (size_t)((const char *)hostDst - (const char *)dst.hostBaseAddress);
+    if (dst.type == HSA_EXT_POINTER_TYPE_HSA)
+        dstAgent = hostDst; /* hipHostMalloc: the same address on every agent */
+    else if (dst.type == HSA_EXT_POINTER_TYPE_LOCKED)
+        dstAgent = (char *)dst.agentBaseAddress + off; /* registered memory: the GPU reaches it at its agent address */
+    else
+        return rtc_fail(RTC_EINVAL, "%s: destination is not page-locked host memory", what);
+    if (off + span > dst.sizeInBytes)
+        return rtc_fail(RTC_EINVAL, "%s: destination range leaves its page-locked allocation", what);
+    gpu = src.agentOwner;
+    cpu = a.cpu[0];
+    hsa_agent_t near{0};
+    if (hsa_agent_get_info(gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NEAREST_CPU, &near) == HSA_STATUS_SUCCESS &&
+        near.handle)
+        cpu = near;
+    return 0;
+}
 } // namespace
 
 extern "C" int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes)
@@ -410,26 +607,198 @@ extern "C" int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes)
         return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: null pointer");
     if (bytes == 0)
         return 0;
-    DmaAgents &a = dma_agents();
-    if (!a.ok)
-        return rtc_fail(RTC_ENODEV, "rtc_copy_d2h_dma: no HSA CPU agent");
-    /* the GPU agent that owns the source, and the destination must be page-locked (hipHostMalloc) memory */
-    hsa_amd_pointer_info_t src{}, dst{};
-    src.size = sizeof(src);
-    dst.size = sizeof(dst);
-    if (hsa_amd_pointer_info(devSrc, &src, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-        src.type != HSA_EXT_POINTER_TYPE_HSA)
-        return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: source is not device memory");
-    if (hsa_amd_pointer_info(hostDst, &dst, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-        (dst.type != HSA_EXT_POINTER_TYPE_HSA && dst.type != HSA_EXT_POINTER_TYPE_LOCKED))
-        return rtc_fail(RTC_EINVAL, "rtc_copy_d2h_dma: destination is not page-locked host memory");
-    thread_local hsa_signal_t sig{0};
-    if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+    hsa_agent_t gpu, cpu;
+    void *dst = nullptr;
+    if (int rc = dma_endpoints(hostDst, bytes, devSrc, "rtc_copy_d2h_dma", gpu, dst, cpu))
+        return rc;
+    thread_local DmaSignal sig;
+    if (!sig.s.handle && hsa_signal_create(1, 0, nullptr, &sig.s) != HSA_STATUS_SUCCESS)
         return rtc_fail(RTC_ENOMEM, "rtc_copy_d2h_dma: hsa_signal_create failed");
-    hsa_signal_store_screlease(sig, 1);
-    if (hsa_amd_memory_async_copy(hostDst, a.cpu[0], devSrc, src.agentOwner, bytes, 0, nullptr, sig) !=
-        HSA_STATUS_SUCCESS)
+    hsa_signal_store_screlease(sig.s, 1);
+    if (hsa_amd_memory_async_copy(dst, cpu, devSrc, gpu, bytes, 0, nullptr, sig.s) != HSA_STATUS_SUCCESS)
         return rtc_fail(RTC_EIO, "rtc_copy_d2h_dma: hsa_amd_memory_async_copy failed");
-    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    return dma_wait(sig.s, "rtc_copy_d2h_dma");
+}
+
+extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void *devSrc, size_t srcPitch,
+                                     size_t rowBytes, int rows)
+{
+    if (rows < 0 || (rows > 0 && rowBytes > 0 && (!hostDst || !devSrc)) || (rows > 1 && (hostPitch < rowBytes ||
+                                                                                         srcPitch < rowBytes)))
+        return rtc_fail(RTC_EINVAL, "rtc_copy_rows_d2h_dma: bad argument");
+    if (rows == 0 || rowBytes == 0)
+        return 0;
+    const size_t span = (size_t)(rows - 1) * hostPitch + rowBytes;
+    hsa_agent_t gpu, cpu;
+    void *dst = nullptr;
+    if (int rc = dma_endpoints(hostDst, span, devSrc, "rtc_copy_rows_d2h_dma", gpu, dst, cpu))
+        return rc;
+    thread_local DmaSignal sig;
+    if (!sig.s.handle && hsa_signal_create(1, 0, nullptr, &sig.s) != HSA_STATUS_SUCCESS)
+        return rtc_fail(RTC_ENOMEM, "rtc_copy_rows_d2h_dma: hsa_signal_create failed");
+    const bool dense = rows == 1 || (hostPitch == rowBytes && srcPitch == rowBytes);
+    const bool aligned4 = (((uintptr_t)dst | (uintptr_t)devSrc | hostPitch | srcPitch | rowBytes) & 3u) == 0;
+    if (dense) {
+        hsa_signal_store_screlease(sig.s, 1);
+        if (hsa_amd_memory_async_copy(dst, cpu, devSrc, gpu, (size_t)rows * rowBytes, 0, nullptr, sig.s) !=
+            HSA_STATUS_SUCCESS)
+            return rtc_fail(RTC_EIO, "rtc_copy_rows_d2h_dma: hsa_amd_memory_async_copy failed");
+    } else if (aligned4) {
+        /* one SDMA sub-window copy: x in bytes, y in rows */
+        hsa_pitched_ptr_t d{dst, hostPitch, hostPitch * (size_t)rows}, sp{const_cast<void *>(devSrc), srcPitch,
+                                                                          srcPitch * (size_t)rows};
+        const hsa_dim3_t zero{0, 0, 0}, range{(uint32_t)rowBytes, (uint32_t)rows, 1};
+        hsa_signal_store_screlease(sig.s, 1);
+        if (hsa_amd_memory_async_copy_rect(&d, &zero, &sp, &zero, &range, gpu, hsaDeviceToHost, 0, nullptr, sig.s) !=
+            HSA_STATUS_SUCCESS)
+            return rtc_fail(RTC_EIO, "rtc_copy_rows_d2h_dma: hsa_amd_memory_async_copy_rect failed");
+    } else {
+        /* rows that are not 4-byte aligned: one linear SDMA copy per row, all on one signal */
+        hsa_signal_store_screlease(sig.s, rows);
+        for (int r = 0; r < rows; ++r)
+            if (hsa_amd_memory_async_copy((char *)dst + (size_t)r * hostPitch, cpu, (const char *)devSrc + (size_t)r * srcPitch,
+                                          gpu, rowBytes, 0, nullptr, sig.s) != HSA_STATUS_SUCCESS) {
+                hsa_signal_subtract_screlease(sig.s, rows - r); /* the copies not issued */
+                (void)dma_wait(sig.s, "rtc_copy_rows_d2h_dma");
+                return rtc_fail(RTC_EIO, "rtc_copy_rows_d2h_dma: hsa_amd_memory_async_copy failed (row %d)", r);
+            }
+    }
+    return dma_wait(sig.s, "rtc_copy_rows_d2h_dma");
+}
+
+extern "C" int rtc_host_register(void *p, size_t bytes)
+{
+    if (!p || !bytes)
+        return rtc_fail(RTC_EINVAL, "rtc_host_register: empty range");
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
     return 0;
+}
+
+extern "C" int rtc_host_unregister(void *p)
+{
+    if (!p)
+        return rtc_fail(RTC_EINVAL, "rtc_host_unregister: null pointer");
+    HIP_TRY(hipHostUnregister(p));
+    return 0;
+}
+
+/* ---- pipelined frames (the host frame loop) -------------------------------------------------------------------
+ * A frame sequence on one device, driven from native code so the per-frame host cost is the launch enqueue alone:
+ * frame k renders the rows of d (RTC_F_OVERLAP: its preparation overlaps frame k-1's sky pass) into devRows[k %
+ * nbuf]; a copy thread waits for the frame's event and moves its rows into hostRows[k % nbuf] (row pitch hostPitch:
+ * a rank's rows y = rowStart + j*rowStride land in the interleaved host frame when hostRows points at row rowStart
+ * and hostPitch = rowStride * width * 3) on the SDMA engines; buffer b is rendered into again once its copy has
+ * finished.  The reference's equivalent is main.c:285-305: the threads write their rows into the shared image, which
+ * stbi_write_bmp then reads. */
+
+extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d,
+                              void *const *devRows, void *const *hostRows, size_t hostPitch, int nbuf, int frames,
+                              void *stream, RtcLoopStats *stats)
+{
+    if (!s || !scene || !cam || !d || !devRows || !hostRows || nbuf <= 0 || nbuf > 16 || frames < 0)
+        return rtc_fail(RTC_EINVAL, "rtc_frame_loop: bad argument");
+    for (int b = 0; b < nbuf; ++b)
+        if (!devRows[b] || !hostRows[b])
+            return rtc_fail(RTC_EINVAL, "rtc_frame_loop: null buffer %d", b);
+    const int rows = rtc_rows_selected(d);
+    const size_t rowBytes = (size_t)(d->width > 0 ? d->width : 0) * 3;
+    if (rows > 1 && hostPitch < rowBytes)
+        return rtc_fail(RTC_EINVAL, "rtc_frame_loop: host pitch %zu < row bytes %zu", hostPitch, rowBytes);
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    RtcRenderDesc dd = *d;
+    dd.flags |= RTC_F_OVERLAP;
+    Events evs;
+    std::vector<hipEvent_t> ready(nbuf);
+    for (int b = 0; b < nbuf; ++b) {
+        HIP_TRY(hipEventCreateWithFlags(&ready[b], hipEventDisableTiming));
+        evs.ev.push_back(ready[b]);
+    }
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<int> jobs;
+    std::vector<char> busy(nbuf, 0);
+    std::vector<double> copyMs;
+    copyMs.reserve(frames);
+    int err = 0;
+    std::string errMsg;
+    bool done = false;
+    std::thread copier([&] {
+        RtcDeviceGuard g(device);
+        for (;;) {
+            int b;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return done || !jobs.empty(); });
+                if (jobs.empty())
+                    return;
+                b = jobs.front();
+                jobs.pop_front();
+            }
+            int rc = 0;
+            double ms = 0.0;
+            const hipError_t e = hipEventSynchronize(ready[b]);
+            if (e != hipSuccess) {
+                rc = rtc_fail(-(int)e, "rtc_frame_loop: frame event: %s", hipGetErrorString(e));
+            } else {
+                const auto c0 = std::chrono::steady_clock::now();
+                rc = rtc_copy_rows_d2h_dma(hostRows[b], hostPitch, devRows[b], rowBytes, rowBytes, rows);
+                ms = ms_since(c0);
+            }
+            std::lock_guard<std::mutex> lk(m);
+            if (rc && !err) {
+                err = rc;
+                errMsg = rtc_last_error();
+            }
+            copyMs.push_back(ms);
+            busy[b] = 0;
+            cv.notify_all();
+        }
+    });
+    const auto t0 = std::chrono::steady_clock::now();
+    double enqueueMs = 0.0;
+    int rc = 0;
+    for (int k = 0; k < frames && !rc; ++k) {
+        const int b = k % nbuf;
+        {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return !busy[b] || err; });
+            if (err)
+                break;
+            busy[b] = 1;
+        }
+        const auto e0 = std::chrono::steady_clock::now();
+        rc = rtc_scene_set_frame_event(s, ready[b]);
+        if (!rc)
+            rc = rtc_render_rows_async(s, scene, cam, &dd, devRows[b], nullptr, nullptr, stream);
+        enqueueMs += ms_since(e0);
+        if (!rc) {
+            std::lock_guard<std::mutex> lk(m);
+            jobs.push_back(b);
+            cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(m);
+        done = true;
+        cv.notify_all();
+    }
+    copier.join();
+    const double wall = ms_since(t0);
+    if (!rc && err)
+        rc = rtc_fail(err, "%s", errMsg.c_str());
+    if (!rc) { /* the frames are on the host; the scene's unjoined sky pass of the last frame has finished too */
+        const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+        if (e != hipSuccess)
+            rc = rtc_fail(-(int)e, "rtc_frame_loop: %s", hipGetErrorString(e));
+    }
+    if (stats) {
+        std::sort(copyMs.begin(), copyMs.end());
+        stats->wallMs = wall;
+        stats->frames = frames;
+        stats->enqueueMs = enqueueMs;
+        stats->copyMsMedian = copyMs.empty() ? 0.0 : copyMs[copyMs.size() / 2];
+        stats->copyMsMax = copyMs.empty() ? 0.0 : copyMs.back();
+    }
+    return rc;
 }

@@ -124,7 +124,7 @@ struct __attribute__((aligned(64))) DevPrimX {
     float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, q0x, q0y, q0z, dac0, pad[3];
 };
 
-/* ---- triangle clusters for bounce rays (the cooperative heavy-tile path) ------------------------------
+/* ---- triangle clusters for bounce rays (rtc_render_chain) -----------------------------------------------
  * The triangles are grouped into clusters of kClusterSize (spatial median splits, rtc_build_clusters); a
  * bounce ray skips a whole cluster when its half-line provably passes farther from the cluster's bounding
  * ball than any point rayTriangle could report.  Bound (SURVEY Appendix A arithmetic, unit roundoff
@@ -562,9 +562,6 @@ struct RenderParams {
     const unsigned long long *__restrict__ pixMask;  /* per 8x8 tile: pixels with a primary candidate (bit i =
                                                        pixel i, row-major); the others see only the sky */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
-    int *__restrict__ heavy;       /* split launch: [0] heavy tiles, [1] next heavy slot (work counter),
-                                      [2] geometry pixels in pixList */
-    const int *__restrict__ pixList; /* geometry pixels of the heavy tiles, heaviest tile first: tile*64 + bit */
     /* rtc_render_chain's work: kGeoLists sub-lists of geometry pixels (tile*64 + bit), filled by rtc_tile_cull
      * (tile t appends to sub-list t % kGeoLists, one atomic per tile with geometry, spread over kGeoLists
      * counters in separate cache lines); geoCount[l * 32] = entries of sub-list l, zeroed by rtc_prep_primary */
@@ -727,10 +724,6 @@ struct Closest {
  * decides as the reference does. */
 constexpr float kTiny = 8.67361738e-19f; /* 2^-60 */
 
-__device__ __forceinline__ bool maybe_hit(float ua, float va, float da)
-{
-    return !(ua < -kTiny) & !(va < -kTiny) & !(ua + va > 1.00001f) & !(da < 0.00099f);
-}
 
 
 
@@ -776,25 +769,6 @@ __device__ __forceinline__ void primary_exact(const RenderParams &P, V3 dir, con
             if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
                 c.dst = dst;
                 c.idx = base + t;
-            }
-        }
-    }
-}
-
-/* primary_exact with the DevPrimX record at hand (LDS-staged in the cooperative kernel) */
-__device__ __forceinline__ void primary_exact_x(V3 dir, const DevPrimF &F, const DevPrimX &X, int t, Closest &c)
-{
-    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
-        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
-        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
-        if (!(-kEps < det && det < kEps)) {
-            const float invDet = rcp_cr(det); /* IEEE 1.f / det */
-            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
-            const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
-            const float dst = X.dac0 * invDet;
-            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
-                c.dst = dst;
-                c.idx = t;
             }
         }
     }
@@ -1303,7 +1277,7 @@ static_assert(kSegSlots * kSegSlotStride == 256 * 16, "rtc_scene_upload allocate
 
 /* counters (rtc.h RTC_SEGMENT_COUNTERS): [0] calculateRayCollision calls, [1] traced, [2] ray-triangle tests of
  * the accumulated samples, [3] ray-cluster tests, [4] ray-triangle tests of speculative samples that were
- * evaluated but not accumulated (rtc_render_chain / rtc_render_pipe / rtc_render_spec) */
+ * evaluated but not accumulated (rtc_render_chain window lanes off the chain) */
 __device__ __forceinline__ void flush_counters(const RenderParams &P, unsigned segCalls, unsigned segTraced,
                                                unsigned long long segTests, int lane, unsigned segClusters = 0,
                                                unsigned long long segSpec = 0)
@@ -1365,7 +1339,7 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 }
 /* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
-__device__ unsigned long long g_rtc_sect[16]; /* [8..] sample statistics (rtc_render_heavy) */
+__device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
 __shared__ unsigned long long s_rtc_sect[16][8];
 #define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define DSECT_END(v, k)                                                                                        \
@@ -1592,62 +1566,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     flush_counters(P, segCalls, segTraced, segTests, lane);
 }
 
-/* ---- the fused launch: cooperative heavy tiles + sky tiles ------------------------------------------------
- * A 1920x1080 frame of ultracomplex.obj has ~1.3 k tiles (of 32.6 k) whose pixels see geometry.  Those "heavy"
- * tiles run 128+ segment iterations of full 120-triangle tests plus Box-Muller shading per lane, while a sky
- * tile is 64 environment lookups; with one lane per pixel the heavy waves alone set the frame time (a few
- * of them per SIMD, latency-bound, long after the sky waves finished).  In the fused launch every heavy tile
- * gets a whole workgroup and kCoop = 4 lanes per pixel:
- *   - the lanes of a pixel hold identical state (RNG, ray, throughput, sample count) and split each
- *     calculateRayCollision: lane j tests triangles j, j+4, ... (primary segments: the tile's candidates
- *     j, j+4, ... in index order), then an exact (dst, index) lexicographic min across the 4 lanes -- the
- *     reference keeps the first of equal distances (strict `<`, raytracing.c:231), i.e. the lowest index;
- *   - RandomDiretion's three Box-Muller normals (moremath.c:97-108) are evaluated one per lane (every lane
- *     advances the RNG through all six draws; lane j keeps draws 2j, 2j+1) and gathered by shuffles;
- *   - the environment's two powf calls (raytracing.c:153,155) are evaluated one per lane and gathered.
- * Every value is produced by the same operations as in rtc_render_kernel, only on different lanes, so the
- * frame is bit-identical.  Sky tiles are rendered by the remaining workgroups with the sky fast path.
- * Launch slots: [0, H) heavy tiles (heaviest first), [H, H + B) the B 16x16 blocks (sky tiles), rest exit. */
-/* KC (the lanes per pixel, a template parameter of the cooperative heavy kernel): 4 or 8 (RTC_F_COOP4 /
- * RTC_F_COOP8); 8 lanes split the trace further and evaluate the six Box-Muller transcendentals on six lanes. */
 #ifndef RTC_SKY_UNROLL
 #define RTC_SKY_UNROLL 2
 #endif
-constexpr int kCoopMaxTris = kLdsTris; /* scene and candidate records in LDS: <= 33 KB per heavy workgroup */
-
-__global__ __launch_bounds__(1024) void rtc_order_heavy(const unsigned *__restrict__ tileW, int numTiles,
-                                                         int *__restrict__ order, int *__restrict__ heavyOut)
-{
-    __shared__ int cnt[65];
-    __shared__ int heavy;
-    if (threadIdx.x < 65)
-        cnt[threadIdx.x] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
-        if (tileW[i] > 0)
-            atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1); /* bucket 0 = 64 pixels with candidates */
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int off = 0;
-        for (int b = 0; b < 64; ++b) {
-            const int c = cnt[b];
-            cnt[b] = off;
-            off += c;
-        }
-        heavy = off;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < numTiles; i += blockDim.x)
-        if (tileW[i] > 0)
-            order[atomicAdd(&cnt[64 - (int)min(64u, tileW[i])], 1)] = i;
-    for (int i = heavy + threadIdx.x; i < numTiles; i += blockDim.x)
-        order[i] = -1;
-    if (threadIdx.x == 0) {
-        heavyOut[0] = heavy;
-        heavyOut[1] = 0;
-    }
-}
-
 
 /* True when the bounce ray (pos, dir) provably cannot hit any triangle of cluster K (see DevCluster): the
  * half-line's distance to the ball centre exceeds T >= r + eps.  rho = |dir|_1 >= |dir| bounds the eps terms;
@@ -1687,218 +1608,6 @@ __device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, float 
     return culled_by(cluster_terms(pos, K), dir, rho, dd);
 }
 
-/* In-group lane exchanges by DPP (VALU lane moves, no LDS round trip; ds_bpermute costs a wait of ~100
- * cycles each, exposed when few waves share a SIMD).  Groups are KC = 4 or 8 consecutive lanes whose lanes
- * share control flow (the lanes of one pixel). */
-constexpr int kDppXor1 = 0xB1;       /* quad_perm(1,0,3,2) */
-constexpr int kDppXor2 = 0x4E;       /* quad_perm(2,3,0,1) */
-constexpr int kDppHalfMirror = 0x141; /* lane i <- lane 7-i within 8 */
-constexpr int kDppRowShl3 = 0x103;   /* lane i <- lane i+3 within a row of 16 */
-template <int CTRL> __device__ __forceinline__ int dpp_i(int v)
-{
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL> __device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
-/* lane K (< 4) of this lane's group */
-template <int KC, int K> __device__ __forceinline__ float group_lane(float v, int sub)
-{
-    const float q = dpp_f<85 * K>(v); /* quad_perm(K,K,K,K) */
-    if constexpr (KC == 4) {
-        return q;
-    } else {
-        const float m = dpp_f<kDppHalfMirror>(q); /* lanes 4..7 take it from lanes 3..0 */
-        return sub < 4 ? q : m;
-    }
-}
-/* exchange partner for reduction step `step` (0: xor 1, 1: xor 2, 2: the other quad of 8) */
-template <int STEP> __device__ __forceinline__ int group_xchg_i(int v)
-{
-    return dpp_i<STEP == 0 ? kDppXor1 : (STEP == 1 ? kDppXor2 : kDppHalfMirror)>(v);
-}
-template <int KC> __device__ __forceinline__ unsigned group_or(unsigned v)
-{
-    v |= (unsigned)group_xchg_i<0>((int)v);
-    v |= (unsigned)group_xchg_i<1>((int)v);
-    if constexpr (KC == 8)
-        v |= (unsigned)group_xchg_i<2>((int)v);
-    return v;
-}
-template <int STEP> __device__ __forceinline__ void lex_min_step(Closest &c)
-{
-    const float od = __int_as_float(group_xchg_i<STEP>(__float_as_int(c.dst)));
-    const int oi = group_xchg_i<STEP>(c.idx);
-    if (od < c.dst || (od == c.dst && (unsigned)oi < (unsigned)c.idx)) {
-        c.dst = od;
-        c.idx = oi;
-    }
-}
-
-/* Position of the n-th (0-based) set bit of m; m must have more than n set bits. */
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n)
-{
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const unsigned long long low = m & ((1ull << w) - 1ull);
-        const int c = __popcll(low);
-        if (n >= c) {
-            n -= c;
-            pos += w;
-            m >>= w;
-        } else {
-            m = low;
-        }
-    }
-    return pos;
-}
-
-/* Cooperative calculateRayCollision for the kCoop lanes of one pixel (no spheres in the fused launch).
- * The heavy tile's workgroup keeps the scene records and its tile's primary-candidate records in LDS:
- * lane `sub` of a group reads record sub, sub+4, ... (four distinct records per wave instruction, each
- * broadcast to 16 lanes). */
-template <int KC>
-__device__ __forceinline__ Closest coop_trace(const RenderParams &P, V3 pos, V3 dir, bool primarySeg,
-                                              const DevTri *__restrict__ sTri, const DevCluster *__restrict__ sCl,
-                                              const DevPrimF *__restrict__ sPrimF, const DevPrimX *__restrict__ sPrimX,
-                                              const int *__restrict__ sCand,
-                                              int L, int sub, unsigned &testedTris)
-{
-    Closest c{999999.f, -1};
-    testedTris = 0;
-    /* Two passes.  The lanes of a wave test unrelated (ray, record) pairs, so a branch inside the test runs
-     * for the whole wave whenever one lane needs it.  Pass 1 evaluates the exact-safe filter branch-free for
-     * all of this lane's records (at most 64: kLdsTris / KC) and keeps the survivors as bits; pass 2 runs
-     * the reference arithmetic for the survivors only, in index order.  Same operations as primary_test /
-     * general_test. */
-    unsigned long long surv = 0;
-    if (primarySeg) {
-        DSECT_BEGIN(d0);
-        for (int k = sub, b = 0; k < L; k += KC, ++b) {
-            const DevPrimF &F = sPrimF[k];
-            const bool keep = (int)!prim_backfacing(dir, F) & (int)prim_pass(dir, F);
-            surv |= (unsigned long long)keep << b;
-        }
-        while (surv) {
-            const int b = __builtin_ctzll(surv);
-            surv &= surv - 1;
-            const int k = sub + KC * b;
-            primary_exact_x(dir, sPrimF[k], sPrimX[k], sCand[k], c);
-        }
-        DSECT_END(d0, 0);
-    } else {
-        DSECT_BEGIN(d1);
-        /* bounce segment: the clusters a ray may hit (lane sub tests clusters sub, sub+KC, ...; OR over
-         * the group), then the records of those clusters, lane sub taking records sub, sub+KC, ... of each;
-         * survivor bit = cluster * kPer + j.  sTri holds the records in cluster order (pad0 = index). */
-        constexpr int kPer = kClusterSize / KC;
-        const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
-        const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
-        unsigned cm = 0;
-        for (int k = sub; k < P.clusterCount; k += KC)
-            cm |= (unsigned)!(rhoOk && cluster_culled(pos, dir, rho, dd, sCl[k])) << k;
-        cm = group_or<KC>(cm);
-        /* triangles in the clusters kept (only the last cluster has zero records) */
-        testedTris = (unsigned)__popc(cm) * kClusterSize -
-                     ((cm >> (P.clusterCount - 1)) & 1u) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
-        DSECT_END(d1, 1);
-        DSECT_BEGIN(d2);
-        unsigned m = cm;
-        while (m) {
-            const int k = __builtin_ctz(m);
-            m &= m - 1;
-#pragma unroll
-            for (int j = 0; j < kPer; ++j)
-                surv |= (unsigned long long)general_filter(pos, dir, sTri[k * kClusterSize + sub + KC * j])
-                        << (k * kPer + j);
-        }
-        DSECT_END(d2, 2);
-        DSECT_BEGIN(d3);
-        while (surv) {
-            const int b = __builtin_ctzll(surv);
-            surv &= surv - 1;
-            const DevTri &R = sTri[(b / kPer) * kClusterSize + sub + KC * (b % kPer)];
-            general_exact(pos, dir, R, __float_as_int(R.pad0), c);
-        }
-        DSECT_END(d3, 3);
-    }
-    DSECT_BEGIN(d4);
-    /* exact (dst, index) lexicographic minimum over the group */
-    lex_min_step<0>(c);
-    lex_min_step<1>(c);
-    if constexpr (KC == 8)
-        lex_min_step<2>(c);
-    DSECT_END(d4, 4);
-    return c;
-}
-
-/* RandomDiretion (moremath.c:104-108) with the three normals on lanes of the pixel's group.
- * KC = 4: lane k < 3 evaluates normal k (its two draws 2k+1, 2k+2, jumped to directly, see RngJump; the
- * log, sqrt and cos of RandomValueNormalDistrubtion, moremath.c:97-102).  KC >= 8: lane k < 3 evaluates
- * rho_k = (float)sqrt(-2 log u), lane 3 + k cos(theta_k), and lane k forms (float)(rho_k * cos_k): one
- * transcendental per lane instead of two in sequence.  Every lane advances its state by the six draws. */
-template <int KC>
-__device__ __forceinline__ V3 random_direction_coop(unsigned &s, int sub, int groupBase)
-{
-    constexpr RngJump j1 = rng_jump(1), j2 = rng_jump(2), j3 = rng_jump(3), j4 = rng_jump(4), j5 = rng_jump(5),
-                      j6 = rng_jump(6);
-    float n;
-    if constexpr (KC == 4) {
-        const int mine = sub < 3 ? sub : 0;
-        const unsigned aA = mine == 0 ? j1.a : (mine == 1 ? j3.a : j5.a);
-        const unsigned aC = mine == 0 ? j1.c : (mine == 1 ? j3.c : j5.c);
-        const unsigned bA = mine == 0 ? j2.a : (mine == 1 ? j4.a : j6.a);
-        const unsigned bC = mine == 0 ? j2.c : (mine == 1 ? j4.c : j6.c);
-        const float uTheta = rng_value_of_state(s * aA + aC);
-        const float uRho = rng_value_of_state(s * bA + bC);
-#ifdef RTC_FAKE_BM /* timing experiment only: not the reference's value */
-        n = sqrtf(-2.f * __logf(uRho)) * __cosf(6.2831853f * uTheta);
-#else
-        const float theta = (float)(2 * 3.14159265 * (double)uTheta);
-        const float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)uRho));
-        n = (float)((double)rho * rtcmath::cos((double)theta));
-#endif
-    } else {
-        /* lane k < 3: draw 2k+2 (rho); lane 3 <= k < 6: draw 2(k-3)+1 (theta) */
-        const int k = sub < 3 ? sub : (sub < 6 ? sub - 3 : 0);
-        const bool isRho = sub < 3;
-        const unsigned dA = isRho ? (k == 0 ? j2.a : (k == 1 ? j4.a : j6.a)) : (k == 0 ? j1.a : (k == 1 ? j3.a : j5.a));
-        const unsigned dC = isRho ? (k == 0 ? j2.c : (k == 1 ? j4.c : j6.c)) : (k == 0 ? j1.c : (k == 1 ? j3.c : j5.c));
-        const float u = rng_value_of_state(s * dA + dC);
-        double t;
-        if (isRho)
-            t = (double)(float)__builtin_sqrt(-2 * rtcmath::log((double)u));
-        else
-            t = rtcmath::cos((double)(float)(2 * 3.14159265 * (double)u));
-        /* lane k < 3 takes cos_k from lane k + 3 */
-        const long long tb = __double_as_longlong(t);
-        const int lo = dpp_i<kDppRowShl3>((int)(unsigned)tb), hi = dpp_i<kDppRowShl3>((int)(tb >> 32));
-        const double c = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-        n = (float)(t * c); /* valid on lanes 0..2: rho_k * cos_k */
-    }
-    s = s * j6.a + j6.c;
-    (void)groupBase;
-    const float nx = group_lane<KC, 0>(n, sub), ny = group_lane<KC, 1>(n, sub), nz = group_lane<KC, 2>(n, sub);
-    return normalized(V3{nx, ny, nz});
-}
-
-/* getEnvironmentLight (raytracing.c:151-160) with its two powf calls on two lanes of the pixel's group */
-template <int KC>
-__device__ __forceinline__ V3 environment_coop(V3 dir, const EnvParams &s, int sub)
-{
-    const float sky = smoothstep_k<kSkyStep>(-dir.y);
-    const float sunDot = fmax0_ref(dot(dir, s.sun));
-    const bool second = (sub & 1) != 0;
-    const float pw = pow_ref(second ? sunDot : sky, second ? s.focus : 0.35f, s);
-    const float skyGradientT = group_lane<KC, 0>(pw, sub);
-    const float sunPow = group_lane<KC, 1>(pw, sub);
-    const V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
-    const float sun = sunPow * s.intensity;
-    const float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);
-    const float sunMask = dir.y < 0.f ? 1.f : 0.f;
-    const float sv = sun * sunMask;
-    return add(lerp(s.ground, skyGradient, groundToSkyT), V3{sv, sv, sv});
-}
-
 /* LDS writes of this wave visible to its other lanes (the wave is the only user of the region) */
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -1908,7 +1617,7 @@ __device__ __forceinline__ void wave_lds_sync()
 }
 
 /* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile of a 16x16 block; the waves of
- * tiles with primary candidates return at once (rtc_render_heavy renders those).  Few registers, so many
+ * tiles whose pixels all have primary candidates return at once (rtc_render_chain renders those).  Few registers, so many
  * waves per SIMD hide the latency of the environment's double-precision chains. */
 __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const unsigned *__restrict__ tileW)
 {
@@ -1922,7 +1631,7 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
     {
         const int bx = blockIdx.x, by = blockIdx.y;
         /* pixels without a primary candidate: their primary ray misses every triangle (the filter is exact-safe),
-         * so every sample is one segment ending in the sky, in heavy tiles too (rtc_render_heavy skips them) */
+         * so every sample is one segment ending in the sky, in tiles with geometry pixels too (rtc_render_chain takes only the geometry pixels) */
         const int t = wave_tile(bx, by);
         const unsigned long long geo = tileW[t] > 0 ? P.pixMask[t] : 0ull;
         if (geo == ~0ull)
@@ -1989,535 +1698,6 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
     flush_counters(P, segCalls, segTraced, 0ull, lane);
 }
 
-/* Heavy tiles (rtc_render_heavy): a fixed set of persistent workgroups takes the heavy tiles one at a time,
- * heaviest first (rtc_order_heavy), from a work counter, so the launch size does not depend on how many
- * tiles see geometry.  Dynamic LDS: the scene's records, the tile's candidate records and indices
- * (rtc_heavy_lds_bytes). */
-constexpr int kHeavyWorkers = 2048;
-#ifndef RTC_COOP_PRIMARY_LIST
-#define RTC_COOP_PRIMARY_LIST 1
-#endif
-constexpr bool kPrimaryList = RTC_COOP_PRIMARY_LIST != 0;
-__host__ __device__ static inline size_t rtc_heavy_lds_bytes(int triPadded)
-{
-    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX) + sizeof(int)) + 16;
-}
-
-#ifndef RTC_HEAVY_WAVES
-#define RTC_HEAVY_WAVES 1
-#endif
-template <int KC>
-__global__ __launch_bounds__(64 * KC) __attribute__((amdgpu_waves_per_eu(RTC_HEAVY_WAVES))) void rtc_render_heavy(
-    RenderParams P)
-{
-    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
-    __shared__ PowTablesLds sPow;
-    DevTri *sTri = (DevTri *)sDyn;
-    DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
-    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
-    DevPrimX *sPrimX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
-    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat) + sizeof(DevPrimX)));
-    int &sCount = sCand[P.triPadded];
-    __shared__ int sItem;
-    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
-    sPow.fill(threadIdx.x);
-    sPow.attach(P.env);
-    for (int i = threadIdx.x; i < P.triPadded; i += (64 * KC)) /* clusterCount * 8 == triPadded */
-        sTri[i] = P.clTris[i];
-    for (int i = threadIdx.x; i < P.clusterCount; i += (64 * KC))
-        sCl[i] = P.clusters[i];
-    for (int i = threadIdx.x; i < P.triPadded; i += (64 * KC)) { /* shading records by reference index */
-        DevMat m = P.mats[i];
-        const DevTri &t = P.tris[i];
-        m.pad0 = t.nx;
-        m.pad1 = t.ny;
-        m.pad2 = t.nz;
-        sShade[i] = m;
-    }
-#ifdef RTC_DIAG
-    if ((threadIdx.x & 63) < 8)
-        s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-#endif
-    const int lane = threadIdx.x & 63;
-    unsigned segCalls = 0, segTraced = 0, segClusters = 0;
-    unsigned long long segTests = 0;
-    const int heavy = P.heavy[0]; /* rtc_order_heavy: number of heavy tiles; P.heavy[1]: next slot */
-#ifdef RTC_DIAG
-    __shared__ unsigned sIters;
-#endif
-    for (;;) {
-        if (threadIdx.x == 0) {
-            sItem = atomicAdd(&P.heavy[1], 1);
-#ifdef RTC_DIAG
-            sIters = 0;
-#endif
-        }
-        __syncthreads();
-        const int slot = __builtin_amdgcn_readfirstlane(sItem);
-        if (slot >= heavy)
-            break;
-        const int tile = P.order[slot];
-        const int wave = threadIdx.x >> 6;
-#ifdef RTC_DIAG
-        const unsigned long long diagRt0 = __builtin_amdgcn_s_memrealtime();
-        unsigned diagIters = 0, diagHits = 0, diagSamples = 0, diagNon7 = 0, diagZero = 0;
-#endif
-        const int tilesX = P.blocksX * 2;
-        const int tx = tile % tilesX, ty = tile / tilesX;
-        const int sub = lane & (KC - 1);
-        const int groupBase = lane & ~(KC - 1);
-        /* the tile's pixels with primary candidates, packed: wave w takes the (16w + lane/KC)-th of them
-         * (row-major); rtc_render_sky renders the others, and waves past the last one only keep the barriers */
-        const unsigned long long geo = P.pixMask[tile];
-        const int slotPx = wave * (64 / KC) + lane / KC;
-        const bool valid = slotPx < __popcll(geo);
-        const int pi = nth_set_bit(geo, valid ? slotPx : 0); /* pixel of the 8x8 tile, row-major */
-        const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
-        const int y = P.rowStart + r * P.rowStride;
-        const V3 pdir = primary_dir(P, x, y);
-        /* Primary segments visit the tile's candidate list (RTC_COOP_PRIMARY_LIST=0: the cluster path like
-         * bounce segments -- one code path for the wave, but ~3x the triangle tests: measured slower). */
-        unsigned L = 0;
-        if (kPrimaryList) {
-        /* LDS: the tile's primary candidates (index order) and their records */
-        if (wave == 0) {
-            const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
-            int base = 0;
-            for (int w = 0; w < P.maskWords; ++w) {
-                const unsigned long long m = mask[w];
-                if ((m >> lane) & 1ull)
-                    sCand[base + __popcll(m & ((1ull << lane) - 1ull))] = w * 64 + lane;
-                base += __popcll(m);
-            }
-            if (lane == 0)
-                sCount = base;
-        }
-        __syncthreads();
-        L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
-        for (int k = threadIdx.x; k < (int)L; k += (64 * KC))
-        {
-            sPrimF[k] = P.primF[sCand[k]];
-            sPrimX[k] = P.primX[sCand[k]];
-        }
-        __syncthreads();
-        }
-
-        unsigned rng = (unsigned)(x + y * P.width); /* main.c:95 */
-        V3 acc{0.f, 0.f, 0.f};
-        bool alive = valid && P.spp > 0 && P.maxBounce > 0;
-        int sample = 0, bounce = 0;
-        V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
-        Closest primary{999999.f, -1};
-        if (P.hoist && alive) {
-            unsigned nc = 0;
-            primary = coop_trace<KC>(P, pos, dir, kPrimaryList, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
-            segTraced++;
-            segTests += kPrimaryList ? L : nc;
-            segClusters += kPrimaryList ? 0u : (unsigned)P.clusterCount;
-        }
-        while (__any(alive)) {
-#ifdef RTC_DIAG
-            diagIters++;
-#endif
-            DSECT_BEGIN(d7);
-            if (alive) {
-                Closest c;
-                segCalls++;
-                if (P.hoist && bounce == 0) {
-                    c = primary;
-                } else {
-                    unsigned nc = 0;
-                    const bool listed = kPrimaryList && bounce == 0;
-                    c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
-                    segTraced++;
-                    segTests += listed ? L : nc;
-                    segClusters += listed ? 0u : (unsigned)P.clusterCount;
-                }
-                bool endSample;
-                if (c.idx >= 0) {
-                    DSECT_BEGIN(d5);
-                    /* calcColor hit branch, raytracing.c:272-287 */
-                    const V3 hitPoint = add(pos, mul(dir, c.dst));
-                    const DevMat M = sShade[c.idx]; /* material, pad0..2 = the stored normal */
-#ifdef RTC_DIAG
-                    diagHits++;
-#endif
-                    const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
-                    const V3 diffuseDir = normalized(add(normal, random_direction_coop<KC>(rng, sub, groupBase)));
-                    const V3 specularDir = reflect(dir, normal);
-                    dir = lerp(diffuseDir, specularDir, M.smoothness);
-                    pos = hitPoint;
-                    const V3 emitted = mul(color, M.emission);
-                    light = add(light, mulv(emitted, rayColor));
-                    rayColor = mulv(rayColor, color);
-                    const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-                    endSample = p < random_value(rng);
-                    if (!endSample) {
-                        rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
-                        bounce++;
-                        endSample = bounce >= P.maxBounce;
-                    }
-                    DSECT_END(d5, 5);
-                } else {
-                    DSECT_BEGIN(d6);
-                    light = add(light, mulv(environment_coop<KC>(dir, P.env, sub), rayColor));
-                    endSample = true;
-                    DSECT_END(d6, 6);
-                }
-                if (endSample) {
-                    acc = add(acc, mul(light, P.invSpp)); /* main.c:99 */
-                    sample++;
-#ifdef RTC_DIAG
-                    diagSamples++;
-                    diagNon7 += diagHits != 1;
-                    diagZero += diagHits == 0;
-                    diagHits = 0;
-#endif
-                    if (sample >= P.spp) {
-                        alive = false;
-                    } else {
-                        pos = P.origin;
-                        dir = pdir;
-                        rayColor = V3{1.f, 1.f, 1.f};
-                        light = V3{0.f, 0.f, 0.f};
-                        bounce = 0;
-                    }
-                }
-            }
-            DSECT_END(d7, 7);
-        }
-        if (valid && sub == 0) {
-            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(acc.x);
-            P.colors[3 * o + 1] = float_to_u8(acc.y);
-            P.colors[3 * o + 2] = float_to_u8(acc.z);
-            if (P.accum) {
-                P.accum[3 * o] = acc.x;
-                P.accum[3 * o + 1] = acc.y;
-                P.accum[3 * o + 2] = acc.z;
-            }
-        }
-        if (sub != 0) {
-            segCalls = segTraced = segClusters = 0;
-            segTests = 0;
-        }
-#ifdef RTC_DIAG
-        if (lane == 0)
-            atomicMax(&sIters, diagIters);
-        if (valid && sub == 0) { /* per pixel: samples, samples with != 1 hit (!= 7 draws), with 0 hits */
-            atomicAdd(&g_rtc_sect[8], (unsigned long long)diagSamples);
-            atomicAdd(&g_rtc_sect[9], (unsigned long long)diagNon7);
-            atomicAdd(&g_rtc_sect[10], (unsigned long long)diagZero);
-            atomicAdd(&g_rtc_sect[11], 1ull);
-            atomicMax(&g_rtc_sect[12], (unsigned long long)diagNon7);
-        }
-#endif
-        __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
-#ifdef RTC_DIAG
-        if (g_rtc_diag && threadIdx.x == 0) {
-            g_rtc_diag[4 * slot] = diagRt0;
-            g_rtc_diag[4 * slot + 1] = __builtin_amdgcn_s_memrealtime();
-            g_rtc_diag[4 * slot + 2] = sIters;
-            g_rtc_diag[4 * slot + 3] = ((unsigned long long)blockIdx.x << 32) | (unsigned)tile;
-        }
-#endif
-    }
-#ifdef RTC_DIAG
-    if (lane < 8)
-        atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
-#endif
-    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters);
-}
-
-
-/* ---- sample-parallel speculative kernel (rtc_render_spec) ------------------------------------------------
- * A pixel's samples are a chain only through the RNG state (main.c:95-100): sample s starts where sample s-1
- * left it, after 7 draws per hit (6 for RandomDiretion, 1 for the roulette, raytracing.c:276-285).  In the
- * tiles with geometry ~99.4 % of samples take exactly as many draws as the sample before them (the primary
- * ray is the same for every sample, and bounce rays rarely hit again), so the next 64 samples can start
- * together: lane i takes the state of the last validated sample advanced by D*i draws (rng_advance), where D
- * is the draw count of the last validated sample.  After the round every lane up to and including the first
- * one whose own draw count differs from D is correct (its start state assumed only earlier lanes); those
- * samples are accumulated in sample order (main.c:99) and the next round starts after the last of them.
- * Same operations as the reference on every value kept; the frame is bit-identical.  One wave per geometry
- * pixel (rtc_pixel_list), 64 samples per round: a pixel's chain is a few segments long, not 2 x spp. */
-__global__ __launch_bounds__(1024) void rtc_pixel_list(const int *__restrict__ order, const unsigned long long *__restrict__ pixMask,
-                                                       int *__restrict__ heavy, int *__restrict__ list)
-{
-    __shared__ int part[1024];
-    __shared__ int running;
-    const int H = heavy[0];
-    if (threadIdx.x == 0)
-        running = 0;
-    __syncthreads();
-    for (int j0 = 0; j0 < H; j0 += 1024) {
-        const int j = j0 + threadIdx.x;
-        const int tile = j < H ? order[j] : -1;
-        const unsigned long long m = tile >= 0 ? pixMask[tile] : 0ull;
-        const int n = __popcll(m);
-        part[threadIdx.x] = n;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) { /* inclusive scan */
-            const int v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
-            __syncthreads();
-            part[threadIdx.x] += v;
-            __syncthreads();
-        }
-        int w = running + part[threadIdx.x] - n;
-        for (unsigned long long b = m; b; b &= b - 1)
-            list[w++] = tile * 64 + __builtin_ctzll(b);
-        __syncthreads();
-        if (threadIdx.x == 1023)
-            running += part[1023];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        heavy[2] = running;
-        heavy[3] = 0;
-    }
-}
-
-/* Primary segments of the speculative kernel: the tile's candidates (bit-set in global memory, scalar
- * loads) over the primary records staged in the workgroup's LDS, ascending index order (strict `<` ties). */
-__device__ __forceinline__ void primary_listed_lds(V3 dir, Closest &c, const unsigned long long *__restrict__ mask,
-                                                   int maskWords, const DevPrimF *__restrict__ sF,
-                                                   const DevPrimX *__restrict__ sX)
-{
-    for (int w = 0; w < maskWords; ++w) {
-        unsigned long long m = mask[w];
-        while (m) {
-            const int t = w * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            const DevPrimF &F = sF[t];
-            if (!prim_backfacing(dir, F) && prim_pass(dir, F)) {
-                /* the reference's arithmetic (raytracing.c:189-208), as primary_test */
-                const DevPrimX &X = sX[t];
-                if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
-                    const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
-                    const float det = dot(V3{X.abx, X.aby, X.abz}, h);
-                    if (!(-kEps < det && det < kEps)) {
-                        const float invDet = rcp_cr(det); /* IEEE 1.f / det */
-                        const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
-                        const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
-                        const float dst = X.dac0 * invDet;
-                        if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
-                            c.dst = dst;
-                            c.idx = t;
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-/* calculateRayCollision for one lane's bounce ray over the clusters it may reach (see DevCluster) */
-__device__ __forceinline__ Closest trace_clusters(const RenderParams &P, V3 pos, V3 dir, const DevTri *__restrict__ sTri,
-                                                  const DevCluster *__restrict__ sCl, unsigned &tests)
-{
-    Closest c{999999.f, -1};
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
-    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
-    for (int k = 0; k < P.clusterCount; ++k) {
-        if (rhoOk && cluster_culled(pos, dir, rho, dd, sCl[k]))
-            continue;
-        tests += (unsigned)min(kClusterSize, P.triCount - k * kClusterSize);
-        unsigned surv = 0;
-#pragma unroll
-        for (int j = 0; j < kClusterSize; ++j)
-            surv |= (unsigned)general_filter(pos, dir, sTri[k * kClusterSize + j]) << j;
-        while (surv) {
-            const int j = __builtin_ctz(surv);
-            surv &= surv - 1;
-            const DevTri &R = sTri[k * kClusterSize + j];
-            general_exact(pos, dir, R, __float_as_int(R.pad0), c);
-        }
-    }
-    return c;
-}
-
-constexpr int kSpecBlock = 256;
-__global__ __launch_bounds__(kSpecBlock) void rtc_render_spec(RenderParams P)
-{
-    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
-    __shared__ PowTablesLds sPow;
-    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
-    DevTri *sTri = (DevTri *)sDyn;
-    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
-    DevPrimF *sPF = (DevPrimF *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevMat)));
-    DevPrimX *sPX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF)));
-    sPow.fill(threadIdx.x);
-    sPow.attach(P.env);
-    for (int i = threadIdx.x; i < P.triPadded; i += kSpecBlock) { /* clusterCount * 8 == triPadded */
-        sTri[i] = P.clTris[i];
-        sPF[i] = P.primF[i];
-        sPX[i] = P.primX[i];
-    }
-    for (int i = threadIdx.x; i < P.clusterCount; i += kSpecBlock)
-        sCl[i] = P.clusters[i];
-    for (int i = threadIdx.x; i < P.triPadded; i += kSpecBlock) { /* shading records by reference index */
-        DevMat m = P.mats[i];
-        const DevTri &t = P.tris[i];
-        m.pad0 = t.nx;
-        m.pad1 = t.ny;
-        m.pad2 = t.nz;
-        sShade[i] = m;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int items = P.heavy[2];
-    unsigned long long segCalls = 0, segTraced = 0, segTests = 0, segClusters = 0, segSpec = 0;
-    for (;;) {
-        /* one pixel per fetch, heaviest tiles first (P.heavy[3]: the next item) */
-        int it = 0;
-        if (lane == 0)
-            it = atomicAdd(&P.heavy[3], 1);
-        it = __builtin_amdgcn_readfirstlane(it);
-        if (it >= items)
-            break;
-        const int code = __builtin_amdgcn_readfirstlane(P.pixList[it]);
-        const int tile = code >> 6, bit = code & 63;
-        const int tilesX = P.blocksX * 2;
-        const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
-        const int y = P.rowStart + r * P.rowStride;
-        const V3 pdir = primary_dir(P, x, y);
-        const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
-        unsigned L = 0;
-        for (int w = 0; w < P.maskWords; ++w)
-            L += (unsigned)__popcll(mask[w]);
-        Closest prim{999999.f, -1};
-        if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            primary_listed_lds(pdir, prim, mask, P.maskWords, sPF, sPX);
-            if (lane == 0) {
-                segTraced++;
-                segTests += L;
-            }
-        }
-#ifdef RTC_DIAG
-        if (lane == 0)
-            atomicAdd(&g_rtc_sect[15], 1ull); /* pixels */
-        unsigned diagRounds = 0;
-#endif
-        unsigned base = (unsigned)(x + y * P.width); /* main.c:95: the state before sample s0 */
-        unsigned D = 7;                              /* predicted draws per sample */
-        V3 acc{0.f, 0.f, 0.f};
-        for (int s0 = 0; s0 < P.spp && P.maxBounce > 0;) {
-            const int n = min(64, P.spp - s0);
-            const bool act = lane < n;
-            unsigned rng = rng_advance(base, D * (unsigned)lane);
-            const unsigned start = rng;
-            V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
-            int bounce = 0;
-            unsigned draws = 0, calls = 0, traced = 0;
-            unsigned long long rtests = 0, rclusters = 0;
-            bool live = act;
-#ifdef RTC_DIAG
-            if (lane == 0)
-                atomicAdd(&g_rtc_sect[13], 1ull); /* rounds */
-            diagRounds++;
-#endif
-            while (__any(live)) {
-#ifdef RTC_DIAG
-                if (lane == 0)
-                    atomicAdd(&g_rtc_sect[14], 1ull); /* wave iterations */
-#endif
-                if (live) {
-                    Closest c;
-                    calls++;
-                    if (bounce == 0) {
-                        if (P.hoist) {
-                            c = prim;
-                        } else {
-                            c = Closest{999999.f, -1};
-                            primary_listed_lds(dir, c, mask, P.maskWords, sPF, sPX);
-                            traced++;
-                            rtests += L;
-                        }
-                    } else {
-                        unsigned tt = 0;
-                        c = trace_clusters(P, pos, dir, sTri, sCl, tt);
-                        traced++;
-                        rtests += tt;
-                        rclusters += (unsigned)P.clusterCount;
-                    }
-                    bool endSample;
-                    if (c.idx >= 0) {
-                        /* calcColor hit branch, raytracing.c:272-287 */
-                        const V3 hitPoint = add(pos, mul(dir, c.dst));
-                        const DevMat M = sShade[c.idx];
-                        const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
-                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
-                        const V3 specularDir = reflect(dir, normal);
-                        dir = lerp(diffuseDir, specularDir, M.smoothness);
-                        pos = hitPoint;
-                        const V3 emitted = mul(color, M.emission);
-                        light = add(light, mulv(emitted, rayColor));
-                        rayColor = mulv(rayColor, color);
-                        const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-                        endSample = p < random_value(rng);
-                        draws += 7;
-                        if (!endSample) {
-                            rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
-                            bounce++;
-                            endSample = bounce >= P.maxBounce;
-                        }
-                    } else {
-                        light = add(light, mulv(environment(dir, P.env), rayColor));
-                        endSample = true;
-                    }
-                    if (endSample)
-                        live = false;
-                }
-            }
-            /* lanes 0..f are correct: f = the first lane whose sample took other than D draws (or the last) */
-            const unsigned long long bad = __ballot(act && draws != D);
-            const int nv = bad ? min(__builtin_ctzll(bad) + 1, n) : n;
-            if (lane < nv) {
-                segCalls += calls;
-                segTraced += traced;
-                segTests += rtests;
-                segClusters += rclusters;
-            } else if (act) {
-                segSpec += rtests;
-            }
-            for (int j = 0; j < nv; ++j) { /* main.c:99, in sample order */
-                const V3 lj{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.x), j)),
-                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.y), j)),
-                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(light.z), j))};
-                acc = add(acc, mul(lj, P.invSpp));
-            }
-            const unsigned lastStart = (unsigned)__builtin_amdgcn_readlane((int)start, nv - 1);
-            const unsigned lastDraws = (unsigned)__builtin_amdgcn_readlane((int)draws, nv - 1);
-            base = rng_advance(lastStart, lastDraws);
-            /* the primary ray is every sample's: 0 draws if it misses, else mostly one hit (7 draws) */
-            D = lastDraws == 0u ? 0u : 7u;
-            s0 += nv;
-        }
-#ifdef RTC_DIAG
-        if (lane == 0)
-            atomicMax(&g_rtc_sect[12], (unsigned long long)diagRounds); /* max rounds of a pixel */
-#endif
-        if (lane == 0) {
-            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(acc.x);
-            P.colors[3 * o + 1] = float_to_u8(acc.y);
-            P.colors[3 * o + 2] = float_to_u8(acc.z);
-            if (P.accum) {
-                P.accum[3 * o] = acc.x;
-                P.accum[3 * o + 1] = acc.y;
-                P.accum[3 * o + 2] = acc.z;
-            }
-        }
-    }
-    flush_counters(P, (unsigned)segCalls, (unsigned)segTraced, segTests, lane, (unsigned)segClusters, segSpec);
-}
-
-__host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
-{
-    return (size_t)triPadded * (sizeof(DevTri) + sizeof(DevMat) + sizeof(DevPrimF) + sizeof(DevPrimX));
-}
-
-
 /* ---- state-indexed samples (rtc_render_chain, the default for pixels that see geometry) --------------------
  * A pixel's samples are chained only through its RNG state (main.c:95-100), and in the OBJ scenes every sample
  * whose primary ray hits draws exactly 7 values per hit (RandomDiretion's six, moremath.c:104-108, and the
@@ -2533,7 +1713,7 @@ __host__ __device__ static inline size_t rtc_spec_lds_bytes(int triPadded)
  * have no sample with a second hit (sum h = spp), so one window of 64 covers them; the others take a second
  * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
- * Work: one wave per geometry pixel (rtc_pixel_list), statically strided over a fixed grid (no atomics). */
+ * Work: one wave per geometry pixel, from the tile cull's sub-lists (see the kernel). */
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
 constexpr int kChainBlock = 256;
 #ifndef RTC_CHAIN_WORKERS
@@ -3081,246 +2261,6 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
     }
 }
 
-/* ---- two samples in flight per pixel (rtc_render_pipe) ----------------------------------------------------
- * A pixel's samples are chained only through the RNG state (main.c:95-100).  Here each pixel has two 4-lane
- * groups: the current one runs sample n from its known start state, the speculative one runs sample n+1
- * from the current start state advanced by D draws (rng_advance; D = 7, a single hit, or 0 when the primary
- * ray misses).  When the current sample ends, its radiance is accumulated (main.c:99, in sample order) and
- * the speculative sample is kept if and only if it started from exactly the state the current one ended in
- * (then it is the reference's sample n+1, whatever path led there); otherwise it restarts from that state.
- * Every accumulated sample is therefore the reference's; the chain of a pixel is about half as long.  Used
- * for small faithful launches (a rank's share of a multi-GPU frame), where chains, not issue, bound the time. */
-__device__ __forceinline__ int pipe_other_i(int v) { return dpp_i<kDppHalfMirror>(v); } /* lane i <- 7-i of 8 */
-__device__ __forceinline__ float pipe_other_f(float v) { return dpp_f<kDppHalfMirror>(v); }
-
-__global__ __launch_bounds__(512) void rtc_render_pipe(RenderParams P)
-{
-    constexpr int KC = 4, kThreads = 512;
-    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
-    __shared__ PowTablesLds sPow;
-    DevTri *sTri = (DevTri *)sDyn;
-    DevPrimF *sPrimF = (DevPrimF *)(sDyn + (size_t)P.triPadded * sizeof(DevTri));
-    DevMat *sShade = (DevMat *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF)));
-    DevPrimX *sPrimX = (DevPrimX *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat)));
-    int *sCand = (int *)(sDyn + (size_t)P.triPadded * (sizeof(DevTri) + sizeof(DevPrimF) + sizeof(DevMat) + sizeof(DevPrimX)));
-    int &sCount = sCand[P.triPadded];
-    __shared__ int sItem;
-    __shared__ DevCluster sCl[kCoopMaxTris / kClusterSize];
-    sPow.fill(threadIdx.x);
-    sPow.attach(P.env);
-    for (int i = threadIdx.x; i < P.triPadded; i += kThreads)
-        sTri[i] = P.clTris[i];
-    for (int i = threadIdx.x; i < P.clusterCount; i += kThreads)
-        sCl[i] = P.clusters[i];
-    for (int i = threadIdx.x; i < P.triPadded; i += kThreads) {
-        DevMat m = P.mats[i];
-        const DevTri &t = P.tris[i];
-        m.pad0 = t.nx;
-        m.pad1 = t.ny;
-        m.pad2 = t.nz;
-        sShade[i] = m;
-    }
-    const int lane = threadIdx.x & 63;
-    const int sub = lane & (KC - 1);
-    const int groupBase = lane & ~(KC - 1);
-    const int g = (lane >> 2) & 1; /* which of the pixel's two groups */
-    unsigned segCalls = 0, segTraced = 0, segClusters = 0;
-    unsigned long long segTests = 0, segEval = 0;
-    const int heavy = P.heavy[0];
-    for (;;) {
-        if (threadIdx.x == 0)
-            sItem = atomicAdd(&P.heavy[1], 1);
-        __syncthreads();
-        const int slot = __builtin_amdgcn_readfirstlane(sItem);
-        if (slot >= heavy)
-            break;
-        const int tile = P.order[slot];
-        const int wave = threadIdx.x >> 6;
-        const int tilesX = P.blocksX * 2;
-        const int tx = tile % tilesX, ty = tile / tilesX;
-        const unsigned long long geo = P.pixMask[tile];
-        const int slotPx = wave * 8 + lane / 8;
-        const bool valid = slotPx < __popcll(geo);
-        const int pi = nth_set_bit(geo, valid ? slotPx : 0);
-        const int x = tx * 8 + (pi & 7), r = ty * 8 + (pi >> 3);
-        const int y = P.rowStart + r * P.rowStride;
-        const V3 pdir = primary_dir(P, x, y);
-        if (wave == 0) {
-            const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
-            int base = 0;
-            for (int w = 0; w < P.maskWords; ++w) {
-                const unsigned long long m = mask[w];
-                if ((m >> lane) & 1ull)
-                    sCand[base + __popcll(m & ((1ull << lane) - 1ull))] = w * 64 + lane;
-                base += __popcll(m);
-            }
-            if (lane == 0)
-                sCount = base;
-        }
-        __syncthreads();
-        const unsigned L = (unsigned)__builtin_amdgcn_readfirstlane(sCount);
-        for (int k = threadIdx.x; k < (int)L; k += kThreads) {
-            sPrimF[k] = P.primF[sCand[k]];
-            sPrimX[k] = P.primX[sCand[k]];
-        }
-        __syncthreads();
-
-        /* this group's sample */
-        int n = -1;
-        unsigned st0 = 0, rng = 0, draws = 0, calls = 0, traced = 0, tests = 0, clTests = 0;
-        int fin = 1, isCur = g == 0, bounce = 0;
-        V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
-        auto start = [&](int ns, unsigned s0) {
-            if (ns < P.spp) {
-                n = ns;
-                st0 = rng = s0;
-                fin = 0;
-            } else {
-                n = -1;
-                fin = 1;
-            }
-            draws = calls = traced = tests = clTests = 0;
-            bounce = 0;
-            pos = P.origin;
-            dir = pdir;
-            rayColor = V3{1.f, 1.f, 1.f};
-            light = V3{0.f, 0.f, 0.f};
-        };
-        /* the pixel (replicated on its 8 lanes) */
-        V3 acc{0.f, 0.f, 0.f};
-        unsigned pixCalls = 0, pixTraced = 0, pixTests = 0, pixClusters = 0;
-        int committed = 0;
-        bool pixDone = !(valid && P.spp > 0 && P.maxBounce > 0);
-        if (!pixDone) {
-            const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
-            if (g == 0)
-                start(0, seed);
-            else
-                start(1, rng_advance(seed, 7u));
-        }
-        while (__any(!pixDone)) {
-            if (!pixDone && n >= 0 && !fin) {
-                /* one calculateRayCollision + calcColor step of this group's sample (as rtc_render_heavy) */
-                Closest c;
-                calls++;
-                unsigned nc = 0;
-                const bool listed = bounce == 0;
-                c = coop_trace<KC>(P, pos, dir, listed, sTri, sCl, sPrimF, sPrimX, sCand, (int)L, sub, nc);
-                traced++;
-                tests += listed ? L : nc;
-                clTests += listed ? 0u : (unsigned)P.clusterCount;
-                if (sub == 0) /* every test evaluated (accumulated or not); the accumulated ones go to [2] below */
-                    segEval += listed ? L : nc;
-                bool endSample;
-                if (c.idx >= 0) {
-                    const V3 hitPoint = add(pos, mul(dir, c.dst));
-                    const DevMat M = sShade[c.idx];
-                    const V3 normal{M.pad0, M.pad1, M.pad2}, color{M.r, M.g, M.b};
-                    const V3 diffuseDir = normalized(add(normal, random_direction_coop<KC>(rng, sub, groupBase)));
-                    const V3 specularDir = reflect(dir, normal);
-                    dir = lerp(diffuseDir, specularDir, M.smoothness);
-                    pos = hitPoint;
-                    const V3 emitted = mul(color, M.emission);
-                    light = add(light, mulv(emitted, rayColor));
-                    rayColor = mulv(rayColor, color);
-                    const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-                    endSample = p < random_value(rng);
-                    draws += 7;
-                    if (!endSample) {
-                        rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
-                        bounce++;
-                        endSample = bounce >= P.maxBounce;
-                    }
-                } else {
-                    light = add(light, mulv(environment_coop<KC>(dir, P.env, sub), rayColor));
-                    endSample = true;
-                }
-                if (endSample)
-                    fin = 1;
-            }
-            /* the other group's sample (every lane of the wave takes part in the exchange) */
-            const int oN = pipe_other_i(n), oFin = pipe_other_i(fin), oCur = pipe_other_i(isCur);
-            const unsigned oSt0 = (unsigned)pipe_other_i((int)st0), oRng = (unsigned)pipe_other_i((int)rng);
-            const unsigned oDraws = (unsigned)pipe_other_i((int)draws), oCalls = (unsigned)pipe_other_i((int)calls),
-                           oTraced = (unsigned)pipe_other_i((int)traced), oTests = (unsigned)pipe_other_i((int)tests),
-                           oClTests = (unsigned)pipe_other_i((int)clTests);
-            const V3 oLight{pipe_other_f(light.x), pipe_other_f(light.y), pipe_other_f(light.z)};
-            (void)oCur;
-            const bool me = isCur != 0;
-            const int cN = me ? n : oN, cFin = me ? fin : oFin;
-            if (!pixDone && cFin && cN >= 0) {
-                const unsigned cRng = me ? rng : oRng, cDraws = me ? draws : oDraws;
-                const V3 cLight = me ? light : oLight;
-                const int sN = me ? oN : n, sFin = me ? oFin : fin;
-                const unsigned sSt0 = me ? oSt0 : st0, sRng = me ? oRng : rng, sDraws = me ? oDraws : draws;
-                const V3 sLight = me ? oLight : light;
-                acc = add(acc, mul(cLight, P.invSpp)); /* main.c:99: sample cN */
-                pixCalls += me ? calls : oCalls;
-                pixTraced += me ? traced : oTraced;
-                pixTests += me ? tests : oTests;
-                pixClusters += me ? clTests : oClTests;
-                committed++;
-                unsigned e = cRng, D = cDraws == 0u ? 0u : 7u;
-                const bool sValid = sN == cN + 1 && sSt0 == e;
-                if (sValid && sFin) {
-                    acc = add(acc, mul(sLight, P.invSpp)); /* sample cN + 1 */
-                    pixCalls += me ? oCalls : calls;
-                    pixTraced += me ? oTraced : traced;
-                    pixTests += me ? oTests : tests;
-                    pixClusters += me ? oClTests : clTests;
-                    committed++;
-                    e = sRng;
-                    D = sDraws == 0u ? 0u : 7u;
-                    if (g == 0) {
-                        start(sN + 1, e);
-                        isCur = 1;
-                    } else {
-                        start(sN + 2, rng_advance(e, D));
-                        isCur = 0;
-                    }
-                } else if (sValid) {
-                    /* the speculative sample is the current one now; the finished group runs the next */
-                    if (me) {
-                        start(sN + 1, rng_advance(sSt0, D));
-                        isCur = 0;
-                    } else {
-                        isCur = 1;
-                    }
-                } else {
-                    /* mispredicted (or none): the other group restarts sample cN + 1 from the true state */
-                    if (!me) {
-                        start(cN + 1, e);
-                        isCur = 1;
-                    } else {
-                        start(cN + 2, rng_advance(e, D));
-                        isCur = 0;
-                    }
-                }
-                if (committed >= P.spp)
-                    pixDone = true;
-            }
-        }
-        if (valid && g == 0 && sub == 0) {
-            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(acc.x);
-            P.colors[3 * o + 1] = float_to_u8(acc.y);
-            P.colors[3 * o + 2] = float_to_u8(acc.z);
-            if (P.accum) {
-                P.accum[3 * o] = acc.x;
-                P.accum[3 * o + 1] = acc.y;
-                P.accum[3 * o + 2] = acc.z;
-            }
-            segCalls += pixCalls;
-            segTraced += pixTraced;
-            segTests += pixTests;
-            segClusters += pixClusters;
-        }
-        __syncthreads(); /* the next tile overwrites sItem / sCand / sPrimF */
-    }
-    /* discarded = evaluated - accumulated, summed over the wave (u64 wrap-around per lane is exact in the sum) */
-    flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segEval - segTests);
-}
-
 static EnvParams env_of(const Scene &s)
 {
     EnvParams e{};
@@ -3350,13 +2290,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                         d->rowStart, d->rowStride);
     if ((long long)d->width * d->height > (1ll << 31) / 4)
         return rtc_fail(RTC_EINVAL, "frame too large");
-    {
-        const int f = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
-        if (f & (f - 1))
-            return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_COOP4 / COOP8 / PIPE / SPEC are exclusive");
-        if ((d->flags & RTC_F_PIPE) && (d->flags & RTC_F_HOIST_PRIMARY))
-            return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_PIPE runs faithful launches only");
-    }
+    if (d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC))
+        return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_COOP4 / COOP8 / PIPE / SPEC name kernels that were "
+                                    "removed (rtc_render_chain renders every geometry pixel)");
     const int rows = rtc_rows_selected(d);
     if (rows == 0)
         return 0;
@@ -3410,11 +2346,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     /* the tile cull keeps the workgroup's prefilter survivors in LDS (maskWords u64, <= 48 KB: 393,216 triangles);
      * larger scenes render without it (same frame) */
     const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords <= 6144;
-    /* the split launch: every scene for rtc_render_chain, up to kCoopMaxTris triangles for the older heavy
-     * kernels (their scene records live in LDS) */
-    const int forcedHeavy = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
-    const bool fused = cull && !debug && P.sphereCount == 0 && (forcedHeavy == 0 || s->triPadded <= kCoopMaxTris) &&
-                       !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
+    /* the split launch (rtc_render_chain + rtc_render_sky): every triangle-only scene */
+    const bool fused = cull && !debug && P.sphereCount == 0 && !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64);
@@ -3423,10 +2356,24 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
     RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
     const int half = overlap ? s->flip : 0; /* the scratch half this launch writes */
+    /* The hooks are one-shot: this launch records the events armed before it and forgets them, so a later launch
+     * never records an event its caller has since released (rtc_scene_set_geometry_event / _frame_event). */
+    const hipEvent_t geoEvent = s->geoEvent, frameEvent = s->frameEvent;
+    ms->geoEvent = nullptr;
+    ms->frameEvent = nullptr;
+    /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
+     * scratch half.  A launch that is not itself overlapped waits for every such pass before its first kernel:
+     * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
+     * overlapped launch waits for the pass on the half it rewrites here, and for the other half before its
+     * geometry kernel (below). */
+    for (int h = 0; h < 2; ++h)
+        if (s->skyPending[h] && (!overlap || h == half)) {
+            HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[h], 0));
+            ms->skyPending[h] = false;
+        }
     size_t halfBytes = 0;
     if (cull) {
-        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + tiles + blocks + 4) * sizeof(int) +
-                            tiles * 64 * sizeof(int) /* + the geometry pixel list */ +
+        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + blocks + 4) * sizeof(int) +
                             (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int); /* + sub-lists */
         halfBytes = (need + 255) & ~(size_t)255;
         if (2 * halfBytes > s->scratchCap) { /* both halves (hipFree synchronises the device: no pass still reads them) */
@@ -3437,37 +2384,29 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             HIP_TRY(hipMalloc(&ms->scratch, 2 * halfBytes));
             ms->scratchCap = 2 * halfBytes;
         }
-        /* an unjoined sky pass of an earlier RTC_F_OVERLAP launch still reading this half: this launch's stream
-         * waits for it before the half is rewritten */
-        if (s->skyPending[half]) {
-            HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[half], 0));
-            ms->skyPending[half] = false;
-        }
     }
     P.blocksX = (int)grid.x;
     /* (the counter slots are zero here: rtc_scene_upload clears them, rtc_reduce_segments re-zeroes them) */
     bool geoRecorded = false;
     auto finish = [&]() -> int {
-        if (s->geoEvent && !geoRecorded)
-            HIP_TRY(hipEventRecord(s->geoEvent, st));
+        if (geoEvent && !geoRecorded)
+            HIP_TRY(hipEventRecord(geoEvent, st));
         if (dSegments) {
             hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
             HIP_TRY(hipGetLastError());
         }
-        if (s->frameEvent) /* the whole frame is written once `st` reaches here (joined launches) */
-            HIP_TRY(hipEventRecord(s->frameEvent, st));
+        if (frameEvent) /* the whole frame is written once `st` reaches here (joined launches) */
+            HIP_TRY(hipEventRecord(frameEvent, st));
         return 0;
     };
-    /* the heavy-tile kernel of the split launch: rtc_render_chain unless one of the older ones is forced */
-    const int forced = d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC);
-    const bool chain = fused && forced == 0;
+    const bool chain = fused;
     unsigned long long *mask = cull ? (unsigned long long *)(s->scratch + (size_t)half * halfBytes) : nullptr;
     unsigned long long *pixMask = cull ? mask + tiles * (size_t)s->maskWords : nullptr;
     unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
     unsigned *tileW = cull ? weight + blocks : nullptr;
     int *order = cull ? (int *)(tileW + tiles) : nullptr;
     if (chain) {
-        P.geoCount = order + tiles + blocks + 4 + tiles * 64;
+        P.geoCount = order + blocks + 4;
         P.geoList = P.geoCount + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
@@ -3498,21 +2437,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {
-            /* sky tiles on the side stream, concurrently with the heavy tiles on `st`; `st` then waits for both.
-             * The older heavy kernels take the heavy tiles heaviest first (rtc_order_heavy); rtc_render_chain
-             * takes the geometry pixels from the tile cull's sub-lists */
-            int *heavy = order + tiles + blocks;
-            if (!chain)
-                hipLaunchKernelGGL(rtc_order_heavy, dim3(1), dim3(1024), 0, st, tileW, (int)tiles, order, heavy);
-            P.order = order;
-            P.heavy = heavy;
-            const bool spec = forced == RTC_F_SPEC;
-            if (spec) {
-                int *pixList = heavy + 4;
-                hipLaunchKernelGGL(rtc_pixel_list, dim3(1), dim3(1024), 0, st, (const int *)order, (const unsigned long long *)pixMask,
-                                   heavy, pixList);
-                P.pixList = pixList;
-            }
+            /* the split launch: the sky pixels on the side stream, concurrently with rtc_render_chain over the
+             * geometry pixels (the tile cull's sub-lists) on `st`; `st` then waits for both */
             hipStream_t skyStream = RTC_SIDE_STREAM ? s->side : st;
             /* RTC_F_OVERLAP: the previous launch's sky pass (reading the other scratch half) ends before this
              * launch's passes start -- its prep and tile cull above overlapped it -- so that the persistent
@@ -3541,56 +2467,35 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
-            const dim3 workers((unsigned)(tiles < (size_t)kHeavyWorkers ? tiles : kHeavyWorkers));
-            const bool eight = forced == RTC_F_COOP8;
-            const bool pipe = forced == RTC_F_PIPE;
-            if (chain) {
-                if (s->chunkCount <= 1) {
-                    /* the primary filter records join the staged cluster records when the block still fits 4
-                     * per CU */
-                    const size_t rec = (size_t)s->clusterCount * kClusterSize * sizeof(DevTri);
-                    const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
-                    P.chainPrimF = kChainStaticLds + rec + pf <= kChainLdsBudget;
-                    hipLaunchKernelGGL(rtc_render_chain<false>, dim3(kChainWorkers), dim3(kChainBlock),
-                                       rec + (P.chainPrimF ? pf : 0), st, P);
-                }
-                else
-                    hipLaunchKernelGGL(rtc_render_chain<true>, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
-                HIP_TRY(hipGetLastError());
-                if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
-                    HIP_TRY(hipEventRecord(s->evHeavy1, st));
-                if (P.sampleCap > 0) {
-                    const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                    hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
-                }
-                if (s->geoEvent) { /* the geometry pixels are done; the sky pass may still run */
-                    HIP_TRY(hipGetLastError());
-                    HIP_TRY(hipEventRecord(s->geoEvent, st));
-                    geoRecorded = true;
-                }
+            if (s->chunkCount <= 1) {
+                /* the primary filter records join the staged cluster records when the block still fits 4 per CU */
+                const size_t rec = (size_t)s->clusterCount * kClusterSize * sizeof(DevTri);
+                const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
+                P.chainPrimF = kChainStaticLds + rec + pf <= kChainLdsBudget;
+                hipLaunchKernelGGL(rtc_render_chain<false>, dim3(kChainWorkers), dim3(kChainBlock),
+                                   rec + (P.chainPrimF ? pf : 0), st, P);
             }
-            else if (spec)
-                hipLaunchKernelGGL(rtc_render_spec, dim3(kHeavyWorkers), dim3(kSpecBlock), rtc_spec_lds_bytes(s->triPadded), st, P);
-            else if (pipe)
-                hipLaunchKernelGGL(rtc_render_pipe, workers, dim3(512), rtc_heavy_lds_bytes(s->triPadded), st, P);
-            else if (eight)
-                hipLaunchKernelGGL(rtc_render_heavy<8>, workers, dim3(64 * 8), rtc_heavy_lds_bytes(s->triPadded), st, P);
             else
-                hipLaunchKernelGGL(rtc_render_heavy<4>, workers, dim3(64 * 4), rtc_heavy_lds_bytes(s->triPadded), st, P);
+                hipLaunchKernelGGL(rtc_render_chain<true>, dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
             HIP_TRY(hipGetLastError());
-            if (s->timing && !chain)
+            if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
+            if (P.sampleCap > 0) {
+                const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
+                hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
+                HIP_TRY(hipGetLastError());
+            }
+            if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
+                HIP_TRY(hipEventRecord(geoEvent, st));
+                geoRecorded = true;
+            }
             ms->timed = s->timing;
             if (overlap) {
                 /* no join: the frame is complete once the side stream has passed both passes */
-                if (s->geoEvent && !geoRecorded) {
-                    HIP_TRY(hipEventRecord(s->geoEvent, st));
-                    geoRecorded = true;
-                }
                 HIP_TRY(hipEventRecord(s->evGeoDone, st));
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
-                if (s->frameEvent)
-                    HIP_TRY(hipEventRecord(s->frameEvent, s->side));
+                if (frameEvent)
+                    HIP_TRY(hipEventRecord(frameEvent, s->side));
                 ms->flip ^= 1;
                 return 0;
             }
@@ -3598,7 +2503,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
             return finish();
         }
-        const_cast<RtcDeviceScene *>(s)->timed = false;
+        ms->timed = false;
         hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
         P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
     }

@@ -5,7 +5,8 @@ we also assert that no pixel exceeds it, that the traced segment count (paths) i
 the uint8 mismatch count.  Integer / index work (RNG, hit tests, hit distances) is bit-exact.  The device
 powf restates glibc's own algorithm (rtc_math.h), so whole frames are bit-identical to the reference except
 NaN sign bits on height-1 frames (every direction NaN); every shortcut of the GPU path (tile lists, clusters,
-cooperative lanes, hoisting, speculation) is checked bit-exact against its brute-force counterpart.
+reach masks, state-indexed windows, deferred sums, hoisting, pipelined frames) is checked bit-exact against its
+brute-force counterpart.
 """
 from __future__ import annotations
 
@@ -157,42 +158,20 @@ def test_tile_cull_is_bit_exact(name, hoist, gpu_available):
     assert np.array_equal(_bits(a0), _bits(a1)) and np.array_equal(c0, c1)
     assert s0["segments"] == s1["segments"]
     assert s1["tri_tests"] <= s0["tri_tests"]
-    # one lane per pixel (RTC_F_NO_COOP) == 4 cooperating lanes per pixel in tiles that see geometry
+    # one lane per pixel everywhere (RTC_F_NO_COOP, rtc_render_kernel) == the split launch (rtc_render_chain over
+    # the geometry pixels, rtc_render_sky over the rest)
     c2, a2, s2 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "coop": False}),
                            want_accum=True)
     assert np.array_equal(_bits(a1), _bits(a2)) and np.array_equal(c1, c2)
     assert s1["segments"] == s2["segments"]
-    # the sample-parallel speculative kernel (RTC_F_SPEC): same bits, same segment counts
-    c4, a4, s4 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "spec": True}), want_accum=True)
-    assert np.array_equal(_bits(a1), _bits(a4)) and np.array_equal(c1, c4) and s1["segments"] == s4["segments"]
-    # 4 and 8 cooperating lanes per pixel (RTC_F_COOP4 / RTC_F_COOP8): same bits, same counters (primary
-    # segments visit only the tile's candidates even when other pixels of the wave are on later bounces:
-    # fewer tests than one lane per pixel); the default state-indexed kernel accumulates the same samples
-    # with the same culling, so its accumulated-sample test count is the cooperative kernels' exactly; two
-    # samples in flight (RTC_F_PIPE, faithful only): same bits, segments and accumulated tests
-    tests = []
-    for lanes in (4, 8):
-        c3, a3, s3 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "coop_lanes": lanes}),
-                               want_accum=True)
-        assert np.array_equal(_bits(a1), _bits(a3)) and np.array_equal(c1, c3)
-        assert s1["segments"] == s3["segments"] and s3["tri_tests"] <= s2["tri_tests"]
-        tests.append(s3["tri_tests"])
-    assert tests[0] == tests[1]
     if sph is None or len(sph) == 0:
-        # the state-indexed kernel also skips, for first bounces, the records that cannot be hit from the
-        # pixel's primary hit point (aligned_normal): fewer or equal tests
-        assert s1["tri_tests"] <= tests[0] and s4["tri_tests"] == tests[0]
+        # the chain kernel culls bounce clusters and unreachable first-bounce records: fewer or equal tests
+        assert s1["tri_tests"] <= s2["tri_tests"]
     # the state-indexed kernel summing each pixel's samples itself (RTC_F_CHAIN_INLINE) == the deferred pass
     c6, a6, s6 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "chain_inline": True}),
                            want_accum=True)
     assert np.array_equal(_bits(a1), _bits(a6)) and np.array_equal(c1, c6) and s1["segments"] == s6["segments"]
     assert s6["tri_tests"] == s1["tri_tests"]
-    if not hoist:
-        c5, a5, s5 = rt.render(tris, sph, scene, cam, rt.RenderConfig(**{**base.__dict__, "pipe": True}),
-                               want_accum=True)
-        assert np.array_equal(_bits(a1), _bits(a5)) and np.array_equal(c1, c5) and s1["segments"] == s5["segments"]
-        if sph is None or len(sph) == 0:
-            assert s5["tri_tests"] == tests[0]
     print(f"{name} hoist={hoist}: tests {s0['tri_tests']} -> {s1['tri_tests']} (+{s1['discarded_tests']} discarded)")
 
 
@@ -336,7 +315,7 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     ds.close()
 
 
-@pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}, {"coop_lanes": 4}, {"spec": True}])
+@pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}])
 def test_overlapped_frames_bit_exact(variant, gpu_available):
     """RTC_F_OVERLAP (frame pipelining): launches that do not join their sky pass, with the next launch's
     preparation (tile cull into the other scratch half) overlapping it.  Eight frames over three cameras, each
@@ -378,13 +357,12 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
         assert np.array_equal(g.cpu().numpy(), ref[k % 3]), f"frame {k}"
     # one buffer, two cameras back to back: the second frame's geometry pixels are not overwritten by the first
     # frame's late sky pass
-    ev = new_event()
-    ds.set_frame_event(ev.cuda_event)
     for c in (cams[1], cams[2]):
+        ev = new_event()
+        ds.set_frame_event(ev.cuda_event)  # one-shot: armed for each launch
         ds.render_rows_async(scene, c, cfg, bufs[0].data_ptr(), stream=st.cuda_stream)
     ev.synchronize()
     assert np.array_equal(bufs[0].cpu().numpy(), ref[2])
-    ds.set_frame_event(None)
     ds.close()
 
 
@@ -419,11 +397,11 @@ def test_overlap_with_counters_and_mixed_launches(gpu_available):
     ds.close()
 
 
-@pytest.mark.parametrize("variant", [{}, {"coop_lanes": 4}, {"coop_lanes": 8}, {"spec": True}, {"hoist": True},
-                                     {"pipe": True}, {"chain_inline": True}, {"hoist": True, "chain_inline": True}])
+@pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}, {"hoist": True, "chain_inline": True},
+                                     {"coop": False}, {"tile_cull": False}])
 def test_spp_not_multiple_of_64(variant, gpu_available):
-    """spp = 100 (the speculative kernel's two rounds of 64 and 36 samples, the cooperative kernels' chains)
-    against the oracle, bit for bit, with identical segment counts."""
+    """spp = 100 (rtc_render_chain's windows of at most 64 state indices, a second window per pixel) against the
+    oracle, bit for bit, with identical segment counts."""
     tris, tonly = load_tris("complex")
     scene, cam, _ = setup_from_flags({})
     cfg = rt.RenderConfig(48, 30, 100, 10, True, **variant)
@@ -488,7 +466,7 @@ def test_cli_multi_gpu_flag_uses_rccl_path(tmp_path, gpu_available):
 
 def test_full_size_properties(gpu_available):
     """The BASELINE workload (ultracomplex 1920x1080x64): deterministic, hoisting bit-exact, and a row sample
-    of the frame matches the oracle within tolerance with identical paths."""
+    of the frame matches the oracle bit for bit with identical paths."""
     tris, tonly = load_tris("ultracomplex")
     scene, cam, _ = setup_from_flags({})
     cfg = rt.RenderConfig(1920, 1080, 64, 10, True)
@@ -500,12 +478,15 @@ def test_full_size_properties(gpu_available):
     assert np.array_equal(_bits(a1), _bits(a3))
     # 1.0317 segments / sample at 480x270 (same scene, same camera)
     assert 1.02 < s1["segments"] / s1["samples"] < 1.045
-    # row sample vs oracle: rows y = 5 + 48k (23 rows, 2.8 M samples)
+    # row sample vs oracle, bit for bit (floats and u8): rows y = 5 + 48k (23 rows, 2.8 M samples)
     d = RtcRenderDesc(1920, 1080, 64, 10, tonly, 5, 48, 0)
-    _, oacc, oseg = orc.render(tris, None, scene, cam, d, threads=16)
+    ocol, oacc, oseg = orc.render(tris, None, scene, cam, d, threads=16)
     mx, over, exact = _compare(a1[5::48], oacc)
     print(f"1080p x64 row sample: max|d|={mx:.3g} over={over} exact={exact:.5f}")
-    assert over == 0
+    assert np.array_equal(_bits(a1[5::48]), _bits(oacc)) and np.array_equal(c1[5::48], ocol)
+    # the same rows rendered alone take the oracle's paths
+    _, _, sr = rt.render(tris, None, scene, cam, rt.RenderConfig(1920, 1080, 64, 10, True, row_start=5, row_stride=48))
+    assert sr["segments"] == oseg
 
 
 @pytest.mark.parametrize("scene,W,H,spp,row0,stride", [("cube", 1920, 1080, 16, 3, 24),
@@ -528,6 +509,91 @@ def test_full_size_baseline_configs(scene, W, H, spp, row0, stride, gpu_availabl
                            want_accum=True)
     assert np.array_equal(_bits(ar), _bits(oacc)) and sr["segments"] == oseg
     print(f"{scene} {W}x{H}x{spp}: frame {s1['frame_ms']:.3f} ms (render {s1['render_ms']:.3f} ms)")
+
+
+@pytest.mark.parametrize("scene,spp", [("ultracomplex", 64), ("complex", 64), ("ultracomplex", 256)])
+def test_full_size_4k_configs(scene, spp, gpu_available):
+    """BASELINE.json at 3840x2160 -- NS (ultracomplex x64), C4 (complex x64), C5 (ultracomplex x256) -- rendered
+    whole on one GPU (the tile cones, chain windows and deferred slots at 4K sizes; main.c:246 needs a 1 GiB stack
+    for this frame on the CPU): a row sample y = 3 + 90k (24 rows) equals the oracle bit for bit, floats and u8,
+    and the same rows rendered alone take the oracle's paths (equal segment counts)."""
+    tris, tonly = load_tris(scene)
+    sc, cam, _ = setup_from_flags({})
+    W, H, row0, stride = 3840, 2160, 3, 90
+    c1, a1, s1 = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True), want_accum=True)
+    d = RtcRenderDesc(W, H, spp, 10, tonly, row0, stride, 0)
+    ocol, oacc, oseg = orc.render(tris, None, sc, cam, d, threads=16)
+    assert oacc.shape[0] == 24
+    mx, over, exact = _compare(a1[row0::stride], oacc)
+    print(f"{scene} {W}x{H}x{spp}: frame {s1['frame_ms']:.3f} ms; row sample max|d|={mx:.3g} exact={exact:.6f}")
+    assert np.array_equal(_bits(a1[row0::stride]), _bits(oacc)) and np.array_equal(c1[row0::stride], ocol)
+    _, _, sr = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True, row_start=row0, row_stride=stride))
+    assert sr["segments"] == oseg
+    # the whole frame takes the survey's path statistics (SURVEY Appendix C: ~1.03 segments per sample)
+    assert 1.0 < s1["segments"] / s1["samples"] < 1.05
+
+
+def test_overlapped_then_other_launches_same_buffer(gpu_available):
+    """an RTC_F_OVERLAP launch leaves its sky pass running on the side stream.  A following launch
+    that is not overlapped -- a joined split launch, a brute-force (no tile cull) launch, a debug launch -- must
+    not race it: the overlapped frame with camera A, then each of those with camera B into the SAME buffer,
+    equals rtc_render of camera B bit for bit (a stale sky pass of camera A would leave its values behind)."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene = rt.default_scene()
+    cam_a = rt.camera_basis()
+    cam_b = rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1)
+    W, H, spp = 640, 360, 32  # a sky pass long enough to still run when the next launch is enqueued
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    for follow in ({}, {"tile_cull": False}, {"coop": False}, {"debug_bounces": True}, {"hoist": True}):
+        cfg_b = rt.RenderConfig(W, H, spp, 10, True, **follow)
+        ref_b, _, _ = rt.render(tris, None, scene, cam_b, cfg_b)
+        for _ in range(3):
+            ds.render_rows_async(scene, cam_a, rt.RenderConfig(W, H, spp, 10, True, overlap=True), buf.data_ptr(),
+                                 stream=st.cuda_stream)
+            ds.render_rows_async(scene, cam_b, cfg_b, buf.data_ptr(), stream=st.cuda_stream)
+            st.synchronize()  # the follower joined (or waited for) every pass it depends on: its stream suffices
+            assert np.array_equal(buf.cpu().numpy(), ref_b), follow
+    ds.close()
+
+
+def test_frame_event_is_one_shot(gpu_available):
+    """rtc_scene_set_frame_event / _geometry_event arm an event for the next launch only (a launch used
+    to record a released event): arm, launch, release the events, launch again (overlapped and joined) -- no
+    crash, every frame right; and a launch after the armed one does not record it again."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, spp = 1920, 1080, 64
+    ref, _, _ = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    for overlap in (True, False):
+        cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=overlap)
+        ev, geo = torch.cuda.Event(), torch.cuda.Event()
+        ev.record(st)
+        geo.record(st)
+        ds.set_frame_event(ev.cuda_event)
+        ds.set_geometry_event(geo.cuda_event)
+        ds.render_rows_async(scene, cam, cfg, buf.data_ptr(), stream=st.cuda_stream)
+        ev.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), ref)
+        # the next launch (a ~0.5 ms frame) does not record ev: it stays complete while that launch runs
+        ds.render_rows_async(scene, cam, cfg, buf.data_ptr(), stream=st.cuda_stream)
+        assert ev.query()
+        torch.cuda.synchronize()
+        del ev, geo  # hipEventDestroy
+        torch.cuda.synchronize()
+        for _ in range(3):
+            ds.render_rows_async(scene, cam, cfg, buf.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), ref)
+    ds.close()
 
 
 @pytest.mark.parametrize("name", ["suzannes_96x54x4", "suzannes_cam_64x48x2"])
@@ -609,3 +675,108 @@ def test_frame_copies(nbytes, gpu_available):
     assert torch.equal(h1, ref)
     rt.copy_d2h_dma(h2.data_ptr(), src.data_ptr(), nbytes)
     assert torch.equal(h2, ref)
+
+
+def _shm_frame(nbytes):
+    """A host frame in POSIX shared memory (what the ranks of a multi-process job all map), page-locked."""
+    import mmap
+
+    fd = os.open(f"/dev/shm/rtc_test_{os.getpid()}", os.O_CREAT | os.O_RDWR, 0o600)
+    os.ftruncate(fd, nbytes)
+    mm = mmap.mmap(fd, nbytes)
+    os.close(fd)
+    os.unlink(f"/dev/shm/rtc_test_{os.getpid()}")
+    arr = np.frombuffer(mm, np.uint8)
+    rt.host_register(arr.ctypes.data, nbytes)
+    return mm, arr
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (121, 67)])
+def test_strided_row_copies_build_host_frame(W, H, gpu_available):
+    """The multi-GPU host-frame path: ranks' compact rows y = r + k*G (G = 2..8 simulated on one device), each
+    copied by rtc_copy_rows_d2h_dma straight into its places of one host frame (pitch G*W*3; SDMA sub-window copy,
+    or per-row copies when W*3 is not a multiple of 4) -- into hipHostMalloc'd memory and into a registered
+    shared-memory frame -- equal the single-GPU host frame byte for byte (main.c:84, :285-302)."""
+    import torch
+
+    from raytracingc_amd.distributed import rows_per_rank
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(W, H, 4, 10, True)
+    ref, _, _ = rt.render(tris, None, scene, cam, cfg)
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.current_stream()
+    mm, shm = _shm_frame(H * W * 3)
+    try:
+        for G in (2, 3, 4, 8):
+            rows = rows_per_rank(H, G)
+            parts = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
+            for r in range(G):
+                ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, 4, 10, True, row_start=r, row_stride=G),
+                                     parts[r].data_ptr(), stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            pinned = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True)
+            shm[:] = 0
+            for r in range(G):
+                n = len(range(r, H, G))
+                for dst in (pinned.data_ptr(), shm.ctypes.data):
+                    rt.copy_rows_d2h_dma(dst + r * W * 3, G * W * 3, parts[r].data_ptr(), W * 3, W * 3, n)
+            assert np.array_equal(pinned.numpy(), ref), f"G={G} pinned"
+            assert np.array_equal(shm.reshape(H, W, 3), ref), f"G={G} shm"
+    finally:
+        rt.host_unregister(shm.ctypes.data)
+        del shm
+        mm.close()
+        ds.close()
+
+
+@pytest.mark.parametrize("name", ["complex", "ultracomplex"])
+def test_render_multi_host_rows_equals_render(name, gpu_available):
+    """rtc_render_multi with RTC_F_HOST_ROWS (no gather: every device copies its rows into the host frame) ==
+    rtc_render bit for bit, colors and floats, same paths."""
+    tris, tonly = load_tris(name)
+    scene, cam, _ = setup_from_flags({})
+    cfg = rt.RenderConfig(160, 90, 8, 10, True)
+    a, fa, sa = rt.render(tris, None, scene, cam, cfg, want_accum=True)
+    b, fb, sb = rt.render_multi(tris, None, scene, cam, rt.RenderConfig(160, 90, 8, 10, True, host_rows=True),
+                                rt.device_count(), want_accum=True)
+    assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
+    assert sa["segments"] == sb["segments"]
+    assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
+
+
+def test_frame_loop_pipelined_host_frames(gpu_available):
+    """rtc_frame_loop (native pipelined frames: RTC_F_OVERLAP renders, a copy thread moving each frame's rows into
+    host memory with the SDMA engines): every buffer's host frame equals rtc_render's, for the whole frame and for
+    the interleaved rows of G = 3 "ranks" written into one shared host frame."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, spp = 640, 360, 16
+    ref, _, _ = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    dev = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(3)]
+    out = ds.frame_loop(scene, cam, rt.RenderConfig(W, H, spp, 10, True), [d.data_ptr() for d in dev],
+                        [h.data_ptr() for h in host], W * 3, 7, st.cuda_stream)
+    assert out["frames"] == 7 and out["wall_ms"] > 0 and out["copy_ms_median"] > 0
+    for h in host:
+        assert np.array_equal(h.numpy(), ref)
+    G = 3
+    mm, shm = _shm_frame(2 * H * W * 3)
+    try:
+        frames = shm.reshape(2, H, W, 3)
+        for r in range(G):
+            cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
+            ds.frame_loop(scene, cam, cfg, [d.data_ptr() for d in dev[:2]],
+                          [frames[b].ctypes.data + r * W * 3 for b in range(2)], G * W * 3, 4, st.cuda_stream)
+        for b in range(2):
+            assert np.array_equal(frames[b], ref), f"buffer {b}"
+    finally:
+        rt.host_unregister(shm.ctypes.data)
+        del frames, shm
+        mm.close()
+    ds.close()

@@ -12,15 +12,27 @@ from conftest import load_tris  # noqa: E402
 v = sys.argv[1] if len(sys.argv) > 1 else "faithful"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 tris, _ = load_tris("ultracomplex")
+import bench  # noqa: E402  (a bench.py workload name renders that workload)
+
+if v in bench.WORKLOADS:
+    name, W, H, spp = bench.WORKLOADS[v]
+    tris, _ = load_tris(name)
+    cfg = rt.RenderConfig(W, H, spp, 10, True)
+    for _ in range(reps):
+        _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+    print(v, st["render_ms"], "geometry items", st["samples"])
+    sys.exit(0)
 cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True),
        "nocull": rt.RenderConfig(1920, 1080, 64, 10, True, tile_cull=False), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
        "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
        "empty": rt.RenderConfig(1920, 1080, 64, 10, True),
        "share8": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8),
-       "share8c4": rt.RenderConfig(1920, 1080, 64, 10, True, row_stride=8, coop_lanes=4),
+       "fsuzane": rt.RenderConfig(1920, 1080, 64, 10, True),
        "ns4k": rt.RenderConfig(3840, 2160, 64, 10, True)}[v]
 if v == "empty":
     tris = tris[:0]
+if v == "fsuzane":
+    tris, _ = load_tris("fsuzane")
 for _ in range(reps):
     _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
 print(v, st["render_ms"])

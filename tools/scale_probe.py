@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One rank's share of a frame at N GPUs (rows y = r + kN), rendered on one GPU: the per-rank device time that
 bounds strong scaling (the gather of the uint8 parts and the re-interleave come on top).  Not part of the product.
-Usage: scale_probe.py [frames] [W H spp] [kernel: chain|pipe|coop4|overlap]  (overlap: the chain kernel with frame
+Usage: scale_probe.py [frames] [W H spp] [kernel: chain|overlap]  (overlap: the chain kernel with frame
 pipelining, RTC_F_OVERLAP -- the per-frame period of back-to-back frames instead of one frame's latency)"""
 import json
 import os
@@ -18,7 +18,7 @@ from conftest import load_tris  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 kernel = sys.argv[5] if len(sys.argv) > 5 else "chain"
-extra = {"chain": {}, "pipe": {"pipe": True}, "coop4": {"coop_lanes": 4}, "overlap": {"overlap": True}}[kernel]
+extra = {"chain": {}, "overlap": {"overlap": True}}[kernel]
 tris, _ = load_tris("ultracomplex")
 scene, cam = rt.default_scene(), rt.camera_basis()
 ds = rt.DeviceScene(tris, None)
