@@ -28,19 +28,23 @@ $(BUILD):
 $(BUILD)/scene_build.o: $(CSRC)/scene_build.c $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+# header dependencies: explicit below, and generated (-MMD) for anything the explicit lists miss
+HDRS     := $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_bm_tables.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h
+-include $(wildcard $(BUILD)/*.d)
 
-$(BUILD)/rtc_frame.o: $(CSRC)/rtc_frame.hip $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+$(BUILD)/rtc_frame.o: $(CSRC)/rtc_frame.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
 
 $(LIB): $(BUILD)/rtc_render.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl -L/opt/rocm/lib -lhsa-runtime64
 
 # diagnostic variant (per-wave cycle stamps); never the measured product
 DIAGLIB  := $(LIBDIR)/librtc_diag.so
-$(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_internal.h include/rtc.h | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -c $< -o $@
+$(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -MMD -MP -c $< -o $@
 
 $(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -ldl -L/opt/rocm/lib -lhsa-runtime64
@@ -48,7 +52,7 @@ $(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build
 diag: $(DIAGLIB)
 
 # exhaustive GPU check of the exact f32 shortcuts (tests/test_gpu_exact.py)
-$(PROBE): tools/exact_probe.hip $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h | $(BUILD)
+$(PROBE): tools/exact_probe.hip $(HDRS) | $(BUILD)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -ffp-contract=off -std=c++17 $< -o $@
 
 probe: $(PROBE)

@@ -212,7 +212,7 @@ int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes);
  * source GPU. */
 int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void *devSrc, size_t srcPitch, size_t rowBytes,
                           int rows);
-/* Page-lock (hipHostRegister, portable) / release an existing host range so the copies above can target it. */
+/* Page-lock (hsa_amd_memory_lock, every agent) / release an existing host range so the copies above can target it. */
 int rtc_host_register(void *p, size_t bytes);
 int rtc_host_unregister(void *p);
 

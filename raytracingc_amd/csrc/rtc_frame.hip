@@ -24,6 +24,8 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -539,6 +541,30 @@ DmaAgents &dma_agents()
     return a;
 }
 
+/* ranges page-locked by rtc_host_register: host base -> (bytes, the agents' address).  The HSA runtime's pointer
+ * info does not report these host addresses, so the copies look them up here. */
+struct LockedRange {
+    size_t bytes;
+    void *agent;
+};
+std::mutex g_lockedMu;
+std::map<uintptr_t, LockedRange> g_locked;
+
+/* the agents' address of [p, p + span) inside one registered range, or null */
+void *locked_agent_address(const void *p, size_t span)
+{
+    std::lock_guard<std::mutex> lk(g_lockedMu);
+    const uintptr_t a = (uintptr_t)p;
+    auto it = g_locked.upper_bound(a);
+    if (it == g_locked.begin())
+        return nullptr;
+    --it;
+    const uintptr_t off = a - it->first;
+    if (off + span > it->second.bytes)
+        return nullptr;
+    return (char *)it->second.agent + off;
+}
+
 /* one completion signal per calling thread, destroyed with the thread */
 struct DmaSignal {
     hsa_signal_t s{0};
@@ -580,17 +606,18 @@ int dma_endpoints(void *hostDst, size_t span, const void *devSrc, const char *wh
     if (hsa_amd_pointer_info(devSrc, &src, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
         src.type != HSA_EXT_POINTER_TYPE_HSA)
         return rtc_fail(RTC_EINVAL, "%s: source is not device memory", what);
-    if (hsa_amd_pointer_info(hostDst, &dst, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS)
-        return rtc_fail(RTC_EINVAL, "%s: destination is not page-locked host memory", what);
-    const size_t off = (size_t)((const char *)hostDst - (const char *)dst.hostBaseAddress);
-    if (dst.type == HSA_EXT_POINTER_TYPE_HSA)
-        dstAgent = hostDst; /* hipHostMalloc: the same address on every agent */
-    else if (dst.type == HSA_EXT_POINTER_TYPE_LOCKED)
-        dstAgent = (char *)dst.agentBaseAddress + off; /* registered memory: the GPU reaches it at its agent address */
-    else
-        return rtc_fail(RTC_EINVAL, "%s: destination is not page-locked host memory", what);
-    if (off + span > dst.sizeInBytes)
-        return rtc_fail(RTC_EINVAL, "%s: destination range leaves its page-locked allocation", what);
+    const hsa_status_t pi = hsa_amd_pointer_info(hostDst, &dst, nullptr, nullptr, nullptr);
+    if (pi == HSA_STATUS_SUCCESS && (dst.type == HSA_EXT_POINTER_TYPE_HSA || dst.type == HSA_EXT_POINTER_TYPE_LOCKED)) {
+        const size_t off = (size_t)((const char *)hostDst - (const char *)dst.hostBaseAddress);
+        /* hipHostMalloc: the same address on every agent; registered (locked) memory: the GPU reaches it at its
+         * agent address */
+        dstAgent = dst.type == HSA_EXT_POINTER_TYPE_HSA ? hostDst : (void *)((char *)dst.agentBaseAddress + off);
+        if (off + span > dst.sizeInBytes)
+            return rtc_fail(RTC_EINVAL, "%s: destination range leaves its page-locked allocation", what);
+    } else if (!(dstAgent = locked_agent_address(hostDst, span))) {
+        return rtc_fail(RTC_EINVAL, "%s: destination is not page-locked host memory (HSA pointer type %d)", what,
+                        pi == HSA_STATUS_SUCCESS ? (int)dst.type : -1);
+    }
     gpu = src.agentOwner;
     cpu = a.cpu[0];
     hsa_agent_t near{0};
@@ -666,11 +693,20 @@ extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void
     return dma_wait(sig.s, "rtc_copy_rows_d2h_dma");
 }
 
+/* Page-locked through the HSA runtime itself (hsa_amd_memory_lock for every agent), so the range has the LOCKED
+ * pointer type rtc_copy_*_d2h_dma resolve to the GPU's agent address, whatever backs it (e.g. a shared-memory file
+ * mapping every rank of a node maps). */
 extern "C" int rtc_host_register(void *p, size_t bytes)
 {
     if (!p || !bytes)
         return rtc_fail(RTC_EINVAL, "rtc_host_register: empty range");
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
+    if (!dma_agents().ok)
+        return rtc_fail(RTC_ENODEV, "rtc_host_register: no HSA runtime");
+    void *agentPtr = nullptr;
+    if (hsa_amd_memory_lock(p, bytes, nullptr, 0, &agentPtr) != HSA_STATUS_SUCCESS || !agentPtr)
+        return rtc_fail(RTC_EIO, "rtc_host_register: hsa_amd_memory_lock failed");
+    std::lock_guard<std::mutex> lk(g_lockedMu);
+    g_locked[(uintptr_t)p] = LockedRange{bytes, agentPtr};
     return 0;
 }
 
@@ -678,7 +714,12 @@ extern "C" int rtc_host_unregister(void *p)
 {
     if (!p)
         return rtc_fail(RTC_EINVAL, "rtc_host_unregister: null pointer");
-    HIP_TRY(hipHostUnregister(p));
+    {
+        std::lock_guard<std::mutex> lk(g_lockedMu);
+        g_locked.erase((uintptr_t)p);
+    }
+    if (hsa_amd_memory_unlock(p) != HSA_STATUS_SUCCESS)
+        return rtc_fail(RTC_EIO, "rtc_host_unregister: hsa_amd_memory_unlock failed");
     return 0;
 }
 

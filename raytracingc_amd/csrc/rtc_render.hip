@@ -1058,6 +1058,7 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
 struct TileCone {
     double c[4][3];
     double vmin, vmax, eDir;
+    double ivmin, ivmax; /* 1 / vmin, 1 / vmax (cone_range multiplies and widens instead of dividing) */
     bool ok;
 };
 
@@ -1094,6 +1095,8 @@ __device__ TileCone rect_cone(const RenderParams &P, int x0, int x1, int r0, int
     K.vmin = vmin * (1.0 - 1e-12);
     K.vmax = vmax * (1.0 + 1e-12);
     K.eDir = 16.0 * u * S / K.vmin + 4.0 * u;
+    K.ivmin = 1.0 / K.vmin;
+    K.ivmax = 1.0 / K.vmax;
     /* basis components <= 1 (normalized f32 vectors) is assumed by the error bound */
     const bool unitBasis = fabs(P.ex.x) <= 1.0001f && fabs(P.ex.y) <= 1.0001f && fabs(P.ex.z) <= 1.0001f &&
                            fabs(P.ey.x) <= 1.0001f && fabs(P.ey.y) <= 1.0001f && fabs(P.ey.z) <= 1.0001f &&
@@ -1117,8 +1120,12 @@ __device__ __forceinline__ void cone_range(const TileCone &K, double gx, double 
         mx = fmax(mx, a);
         mn = fmin(mn, a);
     }
-    ub = mx >= 0.0 ? mx / K.vmin : mx / K.vmax;
-    lb = mn >= 0.0 ? mn / K.vmax : mn / K.vmin;
+    /* mx / vmin (or / vmax) as a product with the rounded reciprocal: two double roundings, < 2^-51 relative, so
+     * widening by 2^-50 of the magnitude keeps ub above (lb below) the exact quotient -- the bound only loosens */
+    ub = mx * (mx >= 0.0 ? K.ivmin : K.ivmax);
+    lb = mn * (mn >= 0.0 ? K.ivmax : K.ivmin);
+    ub += fabs(ub) * 0x1p-50;
+    lb -= fabs(lb) * 0x1p-50;
 }
 
 /* true: no pixel of the tile can pass prim_backfacing / prim_pass for F */
