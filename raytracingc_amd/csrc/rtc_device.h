@@ -185,7 +185,11 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
     const unsigned s0 = s;
     float v[3];
     bool ok = true;
+#ifdef RTC_BM_SERIAL /* experiment: one normal at a time (fewer live registers, less ILP) */
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int c = 0; c < 3; ++c) {
         const float theta = (float)(2 * 3.14159265 * (double)random_value(s)); /* moremath.c:99 */
         float rho;

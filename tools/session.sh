@@ -12,8 +12,12 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-step bench1 150 python bench.py --steps 50 --warmup 5 --no-cpu-baseline || exit $?
-step one_chain 100 python tools/one_render.py ultracomplex_1080p64 5 || exit $?
-step sections 200 python tools/chain_sections.py || exit $?
-bash tools/profile_workload.sh ultracomplex_1080p64 r03a || exit $?
+step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
+for w in ultracomplex_1080p64 fsuzane_1080p64 ultracomplex_4k64; do
+  for lib in librtc_chainold.so librtc.so librtc_nostage.so librtc_chain3.so; do
+    RTC_LIB_PATH=$R/raytracingc_amd/_lib/$lib step "ab_${w}_${lib%.so}" 150 python bench.py --workload $w --steps 30 --warmup 5 --no-cpu-baseline --no-extras || exit $?
+  done
+done
+RTC_SECTIONS=chain2 step sec_ultracomplex 120 python tools/chain_sections.py ultracomplex || exit $?
+RTC_SECTIONS=chain2 step sec_fsuzane 120 python tools/chain_sections.py fsuzane || exit $?
 echo done
