@@ -223,46 +223,6 @@ def kernel_roofline(name, live_ms, dg, work):
 
 
 # ---- GPU ---------------------------------------------------------------------------------------------
-class SharedFrames:
-    """nbuf host frames [H, W, 3] every rank of the node maps (POSIX shared memory, created by local rank 0),
-    page-locked in each process (rtc_host_register) so the SDMA engines write into them."""
-
-    def __init__(self, name, nbuf, H, W, local, barrier):
-        import mmap
-
-        import numpy as np
-
-        import raytracingc_amd as rt
-
-        self.path = f"/dev/shm/{name}"
-        self.nbytes = nbuf * H * W * 3
-        if local == 0:
-            fd = os.open(self.path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
-            os.ftruncate(fd, self.nbytes)
-            os.close(fd)
-        barrier()
-        fd = os.open(self.path, os.O_RDWR)
-        self.mm = mmap.mmap(fd, self.nbytes)
-        os.close(fd)
-        self.arr = np.frombuffer(self.mm, np.uint8).reshape(nbuf, H, W, 3)
-        self.arr.reshape(-1)[::4096] = 0  # fault the pages in before registering
-        rt.host_register(self.arr.ctypes.data, self.nbytes)
-        self.local = local
-
-    def ptr(self, b):
-        return self.arr[b].ctypes.data
-
-    def close(self, barrier):
-        import raytracingc_amd as rt
-
-        rt.host_unregister(self.arr.ctypes.data)
-        del self.arr
-        self.mm.close()
-        barrier()
-        if self.local == 0 and os.path.exists(self.path):
-            os.unlink(self.path)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -283,7 +243,7 @@ def main():
     import torch.distributed as dist
 
     import raytracingc_amd as rt
-    from raytracingc_amd.distributed import rank_config, rows_per_rank
+    from raytracingc_amd.distributed import SharedHostFrames, rank_config, rows_per_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -336,9 +296,9 @@ def main():
     dev_rows = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     shared = None
     if multi:
-        shared = SharedFrames(f"rtc_bench_{os.environ.get('MASTER_PORT', '0')}", nbuf, H, W, local, barrier)
-        host_ptr = [shared.ptr(b) + rank * W * 3 for b in range(nbuf)]
-        host_frame = lambda b: shared.arr[b]  # noqa: E731
+        shared = SharedHostFrames(f"rtc_bench_{os.environ.get('MASTER_PORT', '0')}", nbuf, H, W, local, barrier)
+        host_ptr = [shared.rank_rows_ptr(b, rank) for b in range(nbuf)]
+        host_frame = lambda b: shared.frames[b]  # noqa: E731
     else:
         host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
         host_ptr = [h.data_ptr() + rank * W * 3 for h in host]

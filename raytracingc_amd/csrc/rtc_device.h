@@ -272,8 +272,11 @@ __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
 {
     const float skyArg = smoothstep_k<kSkyStep>(-dir.y);
     float skyGradientT = 0.f;
+    /* smoothstep's value is +0 .. 1 or NaN (never negative, never -0: clamp01 keeps -0 but (-0)^2 = +0) and the
+     * exponent 0.35 is not special, so glibc's powf takes its positive-x path: that path alone, branch-free */
     if (__any(__float_as_uint(skyArg) != 0u))
-        skyGradientT = pow_ref(skyArg, 0.35f, s);
+        skyGradientT = s.log2tab ? rtcmath::powf_glibc_pos<true>(skyArg, 0.35f, s.log2tab, s.exp2tab)
+                                 : rtcmath::powf_glibc_pos<true>(skyArg, 0.35f);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
     const float sunArg = fmax0_ref(dot(dir, s.sun));
     float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);

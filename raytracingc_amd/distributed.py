@@ -1,4 +1,6 @@
-"""Multi-GPU frame rendering: one process per GPU, rows interleaved across ranks, RCCL gather over xGMI.
+"""Multi-GPU frame rendering: one process per GPU, rows interleaved across ranks; the frame reaches the host through
+every GPU's own link (SharedHostFrames + rtc_frame_loop / rtc_copy_rows_d2h_dma) or is gathered to rank 0's HBM
+with RCCL over xGMI (FrameRenderer).
 
 The reference's only parallelism is the row interleave of its 12 pthreads (main.c:84: thread t renders rows
 y = t, t+12, ...).  Here rank r of G renders rows y = r + k*G into a compact [ceil(H/G), W, 3] uint8 buffer on
@@ -86,3 +88,56 @@ def hip_part_renderer(dev_scene, scene, cam, segments: torch.Tensor | None = Non
                                     segments.data_ptr() if segments is not None else None, stream)
 
     return render_part
+
+
+class SharedHostFrames:
+    """`nbuf` host frames [H, W, 3] uint8 that every rank of a node maps (a POSIX shared-memory file created by local
+    rank 0), page-locked in each process (rtc_host_register) so that each GPU's SDMA engines write its rank's rows
+    straight into their places: rank r's rows y = r + k*G start at frame + r*W*3 with row pitch G*W*3
+    (rtc_copy_rows_d2h_dma, rtc_frame_loop) -- the reference's threads likewise write their rows into one image
+    (main.c:84, :285-302).  `barrier` is the group's barrier; register=False skips the page-locking (CPU tests)."""
+
+    def __init__(self, name: str, nbuf: int, height: int, width: int, local_rank: int, barrier,
+                 register: bool = True):
+        import mmap
+        import os
+
+        import numpy as np
+
+        self.path = f"/dev/shm/{name}"
+        self.nbytes = nbuf * height * width * 3
+        self.width = width
+        self.local = local_rank
+        self.registered = False
+        if local_rank == 0:
+            fd = os.open(self.path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, self.nbytes)
+            os.close(fd)
+        barrier()
+        fd = os.open(self.path, os.O_RDWR)
+        self.mm = mmap.mmap(fd, self.nbytes)
+        os.close(fd)
+        self.frames = np.frombuffer(self.mm, np.uint8).reshape(nbuf, height, width, 3)
+        self.frames.reshape(-1)[::4096] = 0  # fault the pages in before page-locking them
+        if register:
+            from . import host_register
+
+            host_register(self.frames.ctypes.data, self.nbytes)
+            self.registered = True
+
+    def rank_rows_ptr(self, b: int, rank: int) -> int:
+        """Where rank `rank`'s first row (y = rank) of frame buffer b lives; the row pitch is world * W * 3."""
+        return self.frames[b].ctypes.data + rank * self.width * 3
+
+    def close(self, barrier) -> None:
+        import os
+
+        if self.registered:
+            from . import host_unregister
+
+            host_unregister(self.frames.ctypes.data)
+        del self.frames
+        self.mm.close()
+        barrier()
+        if self.local == 0 and os.path.exists(self.path):
+            os.unlink(self.path)

@@ -15,7 +15,8 @@ import torch.multiprocessing as mp
 
 from conftest import load_tris, setup_from_flags
 
-from raytracingc_amd.distributed import (FrameRenderer, interleave_reference, rank_config, rows_per_rank)
+from raytracingc_amd.distributed import (FrameRenderer, SharedHostFrames, interleave_reference, rank_config,
+                                         rows_per_rank)
 
 W, H, SPP = 40, 23, 2
 
@@ -129,3 +130,54 @@ def test_partition_helpers():
     out = interleave_reference(parts, 10)
     for y in range(10):
         assert torch.equal(out[y], parts[y % 3, y // 3])
+
+
+def _shared_worker(rank, world, port, q, name):
+    """Each rank writes its rows y = rank + k*world into the node-shared host frame at row pitch world*W*3 (the numpy
+    strided copy stands in for the SDMA rtc_copy_rows_d2h_dma the GPU path uses), in two frame buffers."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import raytracingc_amd as rt
+
+        frames = SharedHostFrames(name, 2, H, W, rank, dist.barrier, register=False)
+        cfg = rank_config(rt.RenderConfig(W, H, SPP, 10, True), rank, world)
+        part = torch.zeros((rows_per_rank(H, world), W, 3), dtype=torch.uint8)
+        _oracle_part(cfg, part)
+        n = len(range(rank, H, world))
+        for b in range(2):
+            flat = np.frombuffer(frames.mm, np.uint8, count=W * 3 * H, offset=b * H * W * 3)
+            view = np.lib.stride_tricks.as_strided(flat[rank * W * 3:], shape=(n, W * 3), strides=(world * W * 3, 1))
+            view[:] = part[:n].numpy().reshape(n, W * 3)
+            del flat, view  # (no view of the mapping may outlive close())
+        dist.barrier()
+        if rank == 0:
+            q.put(frames.frames.copy())
+        dist.barrier()
+        frames.close(dist.barrier)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_shared_host_frame_rows(world):
+    """The multi-process host-frame layout: every rank's interleaved rows land in one shared frame that equals the
+    single-process frame (SharedHostFrames, bench.py at N > 1)."""
+    import raytracingc_amd as rt
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    name = f"rtc_test_shared_{os.getpid()}_{world}"
+    procs = [ctx.Process(target=_shared_worker, args=(r, world, port, q, name)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = torch.zeros((H, W, 3), dtype=torch.uint8)
+    _oracle_part(rt.RenderConfig(W, H, SPP, 10, True), full)
+    for b in range(2):
+        assert np.array_equal(frames[b], full.numpy())
+    assert not os.path.exists(f"/dev/shm/{name}")
