@@ -123,11 +123,6 @@ struct __attribute__((aligned(64))) DevPrimF { /* 64 B: one s_load_dwordx16 */
 struct __attribute__((aligned(64))) DevPrimX {
     float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, q0x, q0y, q0z, dac0, pad[3];
 };
-/* what hit shading reads of the winning triangle (calcColor, raytracing.c:272-287): its stored normal and material,
- * by reference index; staged in LDS by rtc_render_chain */
-struct __attribute__((aligned(32))) DevShade {
-    float nx, ny, nz, r, g, b, emission, smoothness;
-};
 
 /* ---- triangle clusters for bounce rays (rtc_render_chain) -----------------------------------------------
  * The triangles are grouped into clusters of kClusterSize (spatial median splits, rtc_build_clusters); a
@@ -576,9 +571,9 @@ struct RenderParams {
     int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
+    int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
     int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
     int chainPrimF;                 /* rtc_render_chain stages DevPrimF[triPadded] in LDS */
-    int chainStage;                 /* rtc_render_chain also stages: 1 DevPrimX[triPadded], 2 DevShade[triPadded] */
     unsigned char *__restrict__ colors;
     float *__restrict__ accum;
     unsigned long long *__restrict__ segments; /* [0] calculateRayCollision calls, [1] traced, [2] tri tests */
@@ -759,27 +754,6 @@ __device__ __forceinline__ bool prim_pass(V3 dir, const DevPrimF &F)
     return (dt >= F.c) & (fminf(fminf(ut, vt), wt) >= F.negm);
 }
 
-/* The reference's arithmetic (raytracing.c:189-208) for a primary record the filter keeps. */
-__device__ __forceinline__ void primary_exact(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
-                                              Closest &c)
-{
-    const DevPrimX X = P.primX[t];
-    if (!(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
-        const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
-        const float det = dot(V3{X.abx, X.aby, X.abz}, h);
-        if (!(-kEps < det && det < kEps)) {
-            const float invDet = rcp_cr(det); /* IEEE 1.f / det */
-            const float u = dot(V3{X.s0x, X.s0y, X.s0z}, h) * invDet;
-            const float v = dot(dir, V3{X.q0x, X.q0y, X.q0z}) * invDet;
-            const float dst = X.dac0 * invDet;
-            if (!(u < 0.f || u > 1.f) && !(v < 0.f || u + v > 1.f) && !(dst < kEps) && dst < c.dst) {
-                c.dst = dst;
-                c.idx = base + t;
-            }
-        }
-    }
-}
-
 /* One primary record (see closest_primary). */
 __device__ __forceinline__ void primary_test(const RenderParams &P, V3 dir, const DevPrimF &F, int t, int base,
                                              Closest &c)
@@ -863,24 +837,6 @@ __device__ __forceinline__ void closest_primary_listed(const RenderParams &P, V3
             const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
             primary_test(P, dir, P.primF[t], t, base, c);
-        }
-    }
-}
-
-/* closest_primary_listed with the DevPrimF records staged in LDS (rtc_render_chain): the filter's record
- * is an LDS read instead of a dependent scalar load per candidate; DevPrimX (survivors only) stays global. */
-__device__ __forceinline__ void closest_primary_listed_sf(const RenderParams &P, V3 dir, Closest &c,
-                                                          const unsigned long long *__restrict__ mask,
-                                                          const DevPrimF *__restrict__ sF)
-{
-    for (int w = 0; w < P.maskWords; ++w) {
-        unsigned long long m = mask[w];
-        while (m) {
-            const int t = w * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            const DevPrimF &F = sF[t];
-            if (!prim_backfacing(dir, F) && prim_pass(dir, F))
-                primary_exact(P, dir, F, t, 0, c);
         }
     }
 }
@@ -1753,7 +1709,7 @@ constexpr int kChainWorkers = RTC_CHAIN_WORKERS;
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
 typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef RTC_CHAIN_PAIRS
-#define RTC_CHAIN_PAIRS 512
+#define RTC_CHAIN_PAIRS 1024
 #endif
 struct ChainWaveLds {
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
@@ -1957,15 +1913,19 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     return c;
 }
 
-/* The in-order sums of a batch of this wave's finished pixels (the former separate accumulate pass, fused into the kernel's
- * tail): lane q < n adds item finItem's slots in sample order (main.c:97-100, sequential f32 adds from 0) and
- * quantises (raytracing.c:11-15) into pixel finPix.  The slots were written by this wave: an agent-scope fence
- * orders those stores before these loads. */
-__device__ __forceinline__ void chain_sum_batch(const RenderParams &P, int n, int lane, int finItem, int finPix)
+/* The deferred half of rtc_render_chain's walk: for each geometry pixel with a slot, its accumulated samples'
+ * radiance in sample order (main.c:97-100: acc = acc + calcColor(...) * (1/spp), sequential f32 adds from 0), then
+ * vec3ToColor (raytracing.c:11-15).  One lane per pixel.  (Summing a wave's own pixels at the end of
+ * rtc_render_chain instead, without this launch, measured 0.477 vs 0.430 ms per frame: the waves' serial tails hold
+ * their CUs while the sky pass waits for them.) */
+__global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    if (lane < n) {
-        const SampleSlot *slot = P.sampleBuf + (size_t)finItem * (size_t)P.spp;
+    int items = 0;
+    for (int l = 0; l < kGeoLists; ++l)
+        items += P.geoCount[l * kGeoCountStride];
+    items = min(items, P.sampleCap);
+    for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
+        const SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
         f2 accxy{0.f, 0.f};
         float accz = 0.f;
         if (P.maxBounce > 0) {
@@ -1976,7 +1936,7 @@ __device__ __forceinline__ void chain_sum_batch(const RenderParams &P, int n, in
                 accz = accz + v.z;
             }
         }
-        const size_t o = (size_t)finPix;
+        const size_t o = (size_t)P.itemPix[it];
         P.colors[3 * o] = float_to_u8(accxy.x);
         P.colors[3 * o + 1] = float_to_u8(accxy.y);
         P.colors[3 * o + 2] = float_to_u8(accz);
@@ -1988,11 +1948,12 @@ __device__ __forceinline__ void chain_sum_batch(const RenderParams &P, int n, in
     }
 }
 
-/* Primary segments over the tile's candidates with the filter and exact records in LDS (either may be null: then
- * that record comes from global memory); same operations as closest_primary_listed. */
+/* Primary segments over the tile's candidates (rtc_render_chain) with the filter records staged in LDS (null: from
+ * global memory): the filter's record is an LDS read instead of a dependent scalar load per candidate; DevPrimX
+ * (survivors only) stays global.  Same operations as closest_primary_listed. */
 __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P, V3 dir, Closest &c,
                                                            const unsigned long long *__restrict__ mask,
-                                                           const DevPrimF *__restrict__ sF, const DevPrimX *__restrict__ sX)
+                                                           const DevPrimF *__restrict__ sF)
 {
     for (int w = 0; w < P.maskWords; ++w) {
         unsigned long long m = mask[w];
@@ -2002,7 +1963,7 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
             const DevPrimF F = sF ? sF[t] : P.primF[t];
             if (!prim_backfacing(dir, F) && prim_pass(dir, F) && !(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
                 /* the reference's arithmetic (raytracing.c:189-208) */
-                const DevPrimX X = sX ? sX[t] : P.primX[t];
+                const DevPrimX X = P.primX[t];
                 const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
                 const float det = dot(V3{X.abx, X.aby, X.abz}, h);
                 if (!(-kEps < det && det < kEps)) {
@@ -2020,46 +1981,25 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
     }
 }
 
-/* rtc_render_chain's dynamic LDS: the clustered records (MULTI: none), then -- as far as the block's budget allows
- * (P.chainPrimF, P.chainStage) -- the primary filter records, the primary exact records and the shading records */
+/* rtc_render_chain's dynamic LDS: the clustered records (MULTI: none), then, when the block's budget allows
+ * (P.chainPrimF), the primary filter records.  (Staging the primary exact records and the shading records as well
+ * measured no faster.) */
 struct ChainStage {
     DevTri *rec;
     DevPrimF *primF;
-    DevPrimX *primX;
-    DevShade *shade;
 };
 template <bool MULTI>
 __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigned char *sDyn)
 {
-    ChainStage S{nullptr, nullptr, nullptr, nullptr};
-    unsigned char *q = sDyn;
-    if (!MULTI) {
-        S.rec = (DevTri *)q;
-        q += (size_t)P.clusterCount * kClusterSize * sizeof(DevTri);
-    }
-    if (P.chainPrimF) {
-        S.primF = (DevPrimF *)q;
-        q += (size_t)P.triPadded * sizeof(DevPrimF);
-    }
-    if (P.chainStage & 1) {
-        S.primX = (DevPrimX *)q;
-        q += (size_t)P.triPadded * sizeof(DevPrimX);
-    }
-    if (P.chainStage & 2)
-        S.shade = (DevShade *)q;
+    ChainStage S{nullptr, nullptr};
+    if (!MULTI)
+        S.rec = (DevTri *)sDyn;
+    if (P.chainPrimF)
+        S.primF = (DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
     for (int i = threadIdx.x; S.rec && i < P.clusterCount * kClusterSize; i += kChainBlock)
         S.rec[i] = P.clTris[i];
-    for (int i = threadIdx.x; i < P.triPadded; i += kChainBlock) {
-        if (S.primF)
-            S.primF[i] = P.primF[i];
-        if (S.primX)
-            S.primX[i] = P.primX[i];
-        if (S.shade) {
-            const DevTri &T = P.tris[i];
-            const DevMat &M = P.mats[i];
-            S.shade[i] = DevShade{T.nx, T.ny, T.nz, M.r, M.g, M.b, M.emission, M.smoothness};
-        }
-    }
+    for (int i = threadIdx.x; S.primF && i < P.triPadded; i += kChainBlock)
+        S.primF[i] = P.primF[i];
     return S;
 }
 
@@ -2098,8 +2038,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     constexpr bool counting = COUNT;
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0, segSpec = 0;
-    /* this wave's finished deferred pixels whose in-order sums are pending: lane q holds the q-th */
-    int nFin = 0, finItem = 0, finPix = 0;
 #ifdef RTC_DIAG
     unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
 #endif
@@ -2129,7 +2067,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            closest_primary_listed_lds(P, pdir, prim, mask, S.primF, S.primX);
+            closest_primary_listed_lds(P, pdir, prim, mask, S.primF);
             if (counting && lane == 0) {
                 segTraced++;
                 segTests += L;
@@ -2170,7 +2108,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            closest_primary_listed_lds(P, dir, c, mask, S.primF, S.primX);
+                            closest_primary_listed_lds(P, dir, c, mask, S.primF);
                             if (counting)
                                 tests += L;
                         }
@@ -2193,20 +2131,14 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         hits++;
                         /* calcColor hit branch, raytracing.c:272-287 */
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
-                        DevShade H;
-                        if (S.shade) {
-                            H = S.shade[c.idx];
-                        } else {
-                            const DevTri &T = P.tris[c.idx];
-                            const DevMat &M = P.mats[c.idx];
-                            H = DevShade{T.nx, T.ny, T.nz, M.r, M.g, M.b, M.emission, M.smoothness};
-                        }
-                        const V3 normal{H.nx, H.ny, H.nz}, color{H.r, H.g, H.b};
+                        const DevTri &T = P.tris[c.idx];
+                        const DevMat M = P.mats[c.idx];
+                        const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
                         const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
                         const V3 specularDir = reflect(dir, normal);
-                        dir = lerp(diffuseDir, specularDir, H.smoothness);
+                        dir = lerp(diffuseDir, specularDir, M.smoothness);
                         pos = hitPoint;
-                        const V3 emitted = mul(color, H.emission);
+                        const V3 emitted = mul(color, M.emission);
                         light = add(light, mulv(emitted, rayColor));
                         rayColor = mulv(rayColor, color);
                         const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
@@ -2295,14 +2227,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             DSECT_END(dc7, 7);
         }
         if (deferred) {
-            if (lane == nFin) {
-                finItem = it;
-                finPix = r * P.width + x;
-            }
-            if (++nFin == 64) {
-                chain_sum_batch(P, nFin, lane, finItem, finPix);
-                nFin = 0;
-            }
+            if (lane == 0)
+                P.itemPix[it] = r * P.width + x;
         } else if (lane == 0) {
             const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
             P.colors[3 * o] = float_to_u8(accxy.x);
@@ -2315,8 +2241,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             }
         }
     }
-    if (nFin > 0)
-        chain_sum_batch(P, nFin, lane, finItem, finPix);
 #ifdef RTC_DIAG
     if (lane < 8)
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
@@ -2333,574 +2257,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     if (counting)
         flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
 }
-
-/* ---- streaming state indices (rtc_render_chain3) --------------------------------------------------------------
- * The same state-indexed evaluation as rtc_render_chain (S_j = the sample started from the seed advanced by 7 j draws,
- * the reference's k-th sample is S_{j_k}, j_{k+1} = j_k + h_{j_k}), without windows: a lane that finishes its sample
- * takes the next unassigned state index at once (up to the indices the chain will likely need, and at most kRing
- * beyond the chain's position), so long samples (many bounces) no longer hold 63 idle lanes.  Finished samples wait
- * in a per-wave ring in LDS, indexed by state index, until the walk reaches them; the walk consumes the run of
- * finished one-hit samples at the chain's position with one LDS read and one ballot, a member with h != 1 moves the
- * chain by h, and the lanes still evaluating indices the chain skipped are stopped.  Every accumulated value is still
- * one of the reference's samples from its exact start state (bit-identical frame).
- * Bounce segments: a lane whose segment starts at the pixel's primary hit point p0 uses the per-pixel p0 tables
- * (cluster origin terms, first-bounce reach mask: built once per pixel, not per window); the others cull clusters
- * with the general bound.  The surviving (lane, record) pairs are listed lane-major (a wave prefix sum of the lanes'
- * counts) and run 64 per pass; the owner's ray comes by ds_bpermute, no ray slots in LDS. */
-constexpr int kRing = 64; /* ring slots per wave: state indices [cj, cj + kRing) */
-#ifndef RTC_REFILL_MIN
-#define RTC_REFILL_MIN 24
-#endif
-struct Chain3Lds {
-    float4 cl[kChunkClusters][2];       /* the pixel's p0 tables: cluster origin terms (ClusterTerms), [1].z = the
-                                           cluster's reach mask (bit r: record r can be hit from p0) */
-    unsigned long long key[64];         /* closest hit per lane, (dst bits << 32) | index */
-    float4 ring[kRing];                 /* S_j: radiance * (1/spp) xyz, w = j (int bits) */
-    int ringH[kRing];                   /* h_j */
-    uint4 ringCnt[kRing];               /* S_j's counters: calls, triangle tests, cluster tests */
-    unsigned short pair[RTC_CHAIN_PAIRS]; /* lane | record << 6, lane-major */
-};
-constexpr size_t kChain3StaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(Chain3Lds) + 64;
-
-/* exclusive prefix sum over the wave's 64 lanes and the total, in DPP lane moves (no LDS): inclusive scans of the
- * four 16-lane rows (row_shr 1, 2, 4, 8; lanes shifted in from outside the row read 0), then row_bcast:15 adds
- * row r-1's last lane into rows 1 and 3 and row_bcast:31 lane 31 into rows 2 and 3 */
-template <int CTRL, int ROWS> __device__ __forceinline__ int dpp_add(int v)
-{
-    return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xf, true);
-}
-__device__ __forceinline__ int wave_exclusive_scan(int v, int lane, int &total)
-{
-    (void)lane;
-    int s = dpp_add<0x111, 0xf>(v); /* row_shr:1 */
-    s = dpp_add<0x112, 0xf>(s);     /* row_shr:2 */
-    s = dpp_add<0x114, 0xf>(s);     /* row_shr:4 */
-    s = dpp_add<0x118, 0xf>(s);     /* row_shr:8 */
-    s = dpp_add<0x142, 0xa>(s);     /* row_bcast:15 into rows 1, 3 */
-    s = dpp_add<0x143, 0xc>(s);     /* row_bcast:31 into rows 2, 3 */
-    total = __builtin_amdgcn_readlane(s, 63);
-    return s - v;
-}
-
-/* the real records of cluster c (only the scene's last cluster has zero records at its end) */
-__device__ __forceinline__ unsigned cluster_real_mask(const RenderParams &P, int c)
-{
-    const int real = min(kClusterSize, P.triCount - c * kClusterSize);
-    return real >= kClusterSize ? 0xffu : ((1u << real) - 1u);
-}
-
-/* the pair passes: entry i < n is (lane o, record c0 * 8 + (entry >> 6)); the owner's ray by ds_bpermute (every
- * lane takes part), the exact-safe filter, the reference arithmetic for survivors, an atomic lexicographic minimum
- * into the owner's key */
-template <bool MULTI>
-__device__ __forceinline__ void chain3_passes(const RenderParams &P, int n, int c0, V3 pos, V3 dir,
-                                             const DevTri *__restrict__ sRec, Chain3Lds &W, int lane)
-{
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
-        const unsigned pr = i < n ? W.pair[i] : (unsigned)lane;
-        const int o = (int)(pr & 63u);
-        const V3 rpos{bperm_f(o, pos.x), bperm_f(o, pos.y), bperm_f(o, pos.z)};
-        const V3 rdir{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
-        if (i < n) {
-            const int rec = c0 * kClusterSize + (int)(pr >> 6);
-            const DevTri &R = MULTI ? P.clTris[rec] : sRec[rec];
-            Closest c{999999.f, -1};
-            if (general_filter(rpos, rdir, R))
-                general_exact(rpos, rdir, R, __float_as_int(R.pad0), c);
-            if (c.idx >= 0 && c.dst < 999999.f)
-                atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
-        }
-    }
-}
-
-/* One bounce segment of every alive lane (calculateRayCollision, raytracing.c:216-240).  One loop over the
- * clusters: each lane decides whether its half-line may reach cluster k (useP0: the pixel's p0 terms and reach
- * mask; else the general bound), and the lanes that keep k enter their (lane, record) pairs cluster-major at
- * ballot/mbcnt offsets -- a p0 lane the records the reach mask allows, another lane every real record; a full
- * list is run through the passes and refilled. */
-template <bool MULTI>
-__device__ __forceinline__ Closest chain3_trace(const RenderParams &P, bool alive, bool useP0, V3 pos, V3 dir,
-                                                const DevTri *__restrict__ sRec, Chain3Lds &W, int lane, unsigned &tests)
-{
-    W.key[lane] = kNoHitKey;
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
-    const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
-    tests = 0;
-    const bool anyGen = __any(alive && !useP0), anyP0 = __any(alive && useP0);
-    const int nChunks = MULTI ? P.chunkCount : 1;
-    constexpr int kCap = RTC_CHAIN_PAIRS;
-    for (int h = 0; h < nChunks; ++h) {
-        const int c0 = h * kChunkClusters, nCl = MULTI ? min(kChunkClusters, P.clusterCount - c0) : P.clusterCount;
-        bool in = alive;
-        if (MULTI) {
-            if (alive)
-                in = !(rhoOk && cluster_culled(pos, dir, rho, dd, P.chunks[h]));
-            if (!__ballot(in))
-                continue;
-        }
-        DSECT_BEGIN(dq2);
-        int n = 0;
-        for (int k = 0; k < nCl; ++k) {
-            unsigned r8 = 0;
-            bool keep = false;
-            if (!MULTI && anyP0) {
-                const float4 a = W.cl[k][0], b = W.cl[k][1];
-                r8 = __builtin_amdgcn_readfirstlane(__float_as_int(b.z));
-                if (useP0 && in && r8) {
-                    const ClusterTerms t{V3{a.x, a.y, a.z}, a.w, b.x, b.y};
-                    keep = !culled_by(t, dir, rho, dd); /* useP0 implies rhoOk */
-                }
-            }
-            const unsigned full = cluster_real_mask(P, c0 + k);
-            if (anyGen && !useP0)
-                keep = in && !(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k]));
-            const unsigned long long mP = __ballot(keep && useP0), mG = __ballot(keep && !useP0);
-            if (!(mP | mG))
-                continue;
-            const int perP = __popc(r8), perG = __popc(full);
-            const int cP = (int)__popcll(mP) * perP, cG = (int)__popcll(mG) * perG;
-            if (n + cP + cG > kCap) {
-                wave_lds_sync();
-                DSECT_END(dq2, 2);
-                DSECT_BEGIN(dq4a);
-                chain3_passes<MULTI>(P, n, c0, pos, dir, sRec, W, lane);
-                wave_lds_sync();
-                DSECT_END(dq4a, 4);
-                n = 0;
-            }
-            if (keep) {
-                const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)((useP0 ? mP : mG) >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((unsigned)(useP0 ? mP : mG), 0u));
-                int e = n + (useP0 ? rank * perP : cP + rank * perG);
-                tests += (unsigned)(useP0 ? perP : perG);
-                for (unsigned rm = useP0 ? r8 : full; rm; rm &= rm - 1)
-                    W.pair[e++] = (unsigned short)(lane | ((k * kClusterSize + __builtin_ctz(rm)) << 6));
-            }
-            n += cP + cG;
-        }
-        wave_lds_sync();
-        DSECT_END(dq2, 2);
-        DSECT_BEGIN(dq4);
-        chain3_passes<MULTI>(P, n, c0, pos, dir, sRec, W, lane);
-        wave_lds_sync(); /* the pair list is rewritten by the next chunk */
-        DSECT_END(dq4, 4);
-    }
-    const unsigned long long key = W.key[lane];
-    Closest c{999999.f, -1};
-    if (key != kNoHitKey) {
-        c.dst = __uint_as_float((unsigned)(key >> 32));
-        c.idx = (int)(unsigned)key;
-    }
-    return c;
-}
-
-/* The in-order sums of a batch of this wave's finished pixels (the former separate accumulate pass, fused into the kernel's
- * tail): lane q < n adds item finItem's slots in sample order (main.c:97-100, sequential f32 adds from 0) and
- * quantises (raytracing.c:11-15) into pixel finPix.  The slots were written by this wave: an agent-scope fence
- * orders those stores before these loads. */
-__device__ __forceinline__ void chain3_sum_batch(const RenderParams &P, int n, int lane, int finItem, int finPix)
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    if (lane < n) {
-        const SampleSlot *slot = P.sampleBuf + (size_t)finItem * (size_t)P.spp;
-        f2 accxy{0.f, 0.f};
-        float accz = 0.f;
-        if (P.maxBounce > 0) {
-#pragma unroll 8
-            for (int k = 0; k < P.spp; ++k) {
-                const SampleSlot v = slot[k];
-                accxy = accxy + f2{v.x, v.y};
-                accz = accz + v.z;
-            }
-        }
-        const size_t o = (size_t)finPix;
-        P.colors[3 * o] = float_to_u8(accxy.x);
-        P.colors[3 * o + 1] = float_to_u8(accxy.y);
-        P.colors[3 * o + 2] = float_to_u8(accz);
-        if (P.accum) {
-            P.accum[3 * o] = accxy.x;
-            P.accum[3 * o + 1] = accxy.y;
-            P.accum[3 * o + 2] = accz;
-        }
-    }
-}
-
-/* COUNT: the launch asks for segment counters (instrumentation, untimed); without it the counters are compiled out */
-template <bool MULTI, bool COUNT>
-__global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain3(
-    RenderParams P)
-{
-    extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
-    __shared__ PowTablesLds sPow;
-    __shared__ Chain3Lds sWave[kChainBlock / 64];
-    __shared__ int sWork;
-    if (threadIdx.x == 0)
-        sWork = 0;
-    DevTri *sRec = MULTI ? nullptr : (DevTri *)sDyn;
-    DevPrimF *sPrimF = (!MULTI && P.chainPrimF) ? (DevPrimF *)(sRec + P.clusterCount * kClusterSize) : nullptr;
-    sPow.fill(threadIdx.x);
-    if (!MULTI)
-        for (int i = threadIdx.x; i < P.clusterCount * kClusterSize; i += kChainBlock)
-            sRec[i] = P.clTris[i];
-    if (sPrimF)
-        for (int i = threadIdx.x; i < P.triPadded; i += kChainBlock)
-            sPrimF[i] = P.primF[i];
-#ifdef RTC_DIAG
-    if ((threadIdx.x & 63) < 8)
-        s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-#endif
-    __syncthreads();
-    sPow.attach(P.env);
-    const int lane = threadIdx.x & 63;
-    Chain3Lds &W = sWave[threadIdx.x >> 6];
-    const RngJump laneJump = rng_jump_by(7u * (unsigned)lane); /* J(7 lane): s -> the state 7 lane draws later */
-    constexpr RngJump kJump7 = rng_jump(7);
-    int nextIt = 0;
-    if (lane == 0)
-        nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
-    const int tilesX = P.blocksX * 2;
-    constexpr bool counting = COUNT;
-    unsigned segCalls = 0, segTraced = 0, segClusters = 0;
-    unsigned long long segTests = 0, segSpec = 0;
-    /* this wave's finished deferred pixels whose in-order sums are pending: lane q holds the q-th */
-    int nFin = 0, finItem = 0, finPix = 0;
-#ifdef RTC_DIAG
-    unsigned long long dIters = 0, dBusy = 0, dAssigned = 0, dPixels = 0, dPrim = 0;
-#endif
-    int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
-    for (;;) {
-        const int it = __builtin_amdgcn_readfirstlane(nextIt);
-        while (it - base >= cnt && l < kGeoLists - 1) {
-            base += cnt;
-            ++l;
-            cnt = __builtin_amdgcn_readfirstlane(P.geoCount[l * kGeoCountStride]);
-        }
-        if (it - base >= cnt)
-            break;
-        if (lane == 0)
-            nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
-        const int code = __builtin_amdgcn_readfirstlane(P.geoList[(size_t)l * P.geoCap + (it - base)]);
-        const int tile = code >> 6, bit = code & 63;
-        const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
-        const int y = P.rowStart + r * P.rowStride;
-        const V3 pdir = primary_dir(P, x, y); /* main.c:88-94 */
-        const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
-        unsigned L = 0;
-        for (int w = 0; w < P.maskWords; ++w)
-            L += (unsigned)__popcll(mask[w]);
-        const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
-        const bool deferred = it < P.sampleCap; /* wave-uniform */
-        SampleSlot *slots = P.sampleBuf + (size_t)it * (size_t)P.spp;
-        Closest prim{999999.f, -1};
-        bool primKnown = false; /* the primary hit is known (tables built) */
-        if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            if (sPrimF)
-                closest_primary_listed_sf(P, pdir, prim, mask, sPrimF);
-            else
-                closest_primary_listed(P, pdir, prim, 0, mask);
-            if (counting && lane == 0) {
-                segTraced++;
-                segTests += L;
-            }
-        }
-        W.ring[lane].w = __int_as_float(-1); /* kRing == 64: one slot per lane */
-        f2 accxy{0.f, 0.f}; /* the pixel's accumulator (main.c:97): x, y packed, z */
-        float accz = 0.f;
-        int k = 0;          /* samples accumulated */
-        unsigned cj = 0;    /* the chain's position: state index of sample k */
-        unsigned nextJ = 0; /* next state index to assign */
-        unsigned sNext = seed; /* the RNG state at index nextJ (the seed advanced by 7 nextJ draws) */
-        bool busy = false, seg0 = false, fromP0 = false;
-        unsigned myJ = 0, rng = 0, hits = 0, calls = 0, tests = 0, clTests = 0;
-        int bounce = 0;
-        V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
-        while (k < P.spp && P.maxBounce > 0) {
-            /* ---- assign the next state indices to the free lanes ---- */
-            DSECT_BEGIN(dq0);
-            {
-                /* the state indices the remaining samples likely span: need x (indices per sample so far), no
-                 * margin (a margin makes every pixel evaluate samples it never uses); lanes are refilled once at
-                 * least RTC_REFILL_MIN are free, or when none is busy (each refill costs a faithful primary trace) */
-                const int need = P.spp - k;
-                const int est = k > 0 ? (int)(((unsigned long long)need * cj + (unsigned)k - 1u) / (unsigned)k) : need;
-                const unsigned lim = cj + (unsigned)min(kRing, est);
-                const unsigned long long freeM = __ballot(!busy);
-                const int nFree = (int)__popcll(freeM);
-                const int na = (lim > nextJ && (nFree >= RTC_REFILL_MIN || nFree == 64)) ? min((int)(lim - nextJ), nFree) : 0;
-                if (na > 0) {
-                    const unsigned s0 = sNext; /* the state at index nextJ */
-                    const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(freeM >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)freeM, 0u));
-                    /* lane `rank`'s constant jump J(7 rank) (every lane takes part in the permutes) */
-                    const unsigned ja = (unsigned)__builtin_amdgcn_ds_bpermute((rank & 63) << 2, (int)laneJump.a);
-                    const unsigned jc = (unsigned)__builtin_amdgcn_ds_bpermute((rank & 63) << 2, (int)laneJump.c);
-                    /* the state at index nextJ + na: J(7 na) = J(7 (na - 1)) then J(7) */
-                    const unsigned na1a = (unsigned)__builtin_amdgcn_readlane((int)laneJump.a, na - 1);
-                    const unsigned na1c = (unsigned)__builtin_amdgcn_readlane((int)laneJump.c, na - 1);
-                    sNext = (s0 * na1a + na1c) * kJump7.a + kJump7.c;
-                    if (!busy && rank < na) {
-                        rng = s0 * ja + jc;
-                        myJ = nextJ + (unsigned)rank;
-                        busy = true;
-                        seg0 = true;
-                        fromP0 = false;
-                        pos = P.origin;
-                        dir = pdir;
-                        rayColor = V3{1.f, 1.f, 1.f};
-                        light = V3{0.f, 0.f, 0.f};
-                        bounce = 0;
-                        hits = calls = tests = clTests = 0;
-                    }
-                    nextJ += (unsigned)na;
-#ifdef RTC_DIAG
-                    dAssigned += (unsigned)na;
-#endif
-                }
-            }
-            DSECT_END(dq0, 0);
-#ifdef RTC_DIAG
-            dIters++;
-            dBusy += (unsigned long long)__popcll(__ballot(busy));
-            dPrim += __any(busy && seg0) ? 1u : 0u;
-#endif
-            /* ---- one segment of every busy lane: primary (uniform) and/or bounce (pairs) ---- */
-            Closest c{999999.f, -1};
-            DSECT_BEGIN(dq1);
-            if (__any(busy && seg0)) {
-                Closest cp = prim;
-                if (!P.hoist) {
-                    cp = Closest{999999.f, -1};
-                    if (sPrimF)
-                        closest_primary_listed_sf(P, pdir, cp, mask, sPrimF);
-                    else
-                        closest_primary_listed(P, pdir, cp, 0, mask);
-                }
-                if (!primKnown) {
-                    primKnown = true;
-                    /* the pixel's p0 tables: every first bounce starts at the primary hit point p0 */
-                    if (!MULTI && P.clusterCull && cp.idx >= 0) {
-                        const V3 p0 = add(P.origin, mul(pdir, cp.dst)); /* raytracing.c:238 */
-                        unsigned long long reach[kChunkClusters * kClusterSize / 64];
-#pragma unroll
-                        for (int q = 0; q < kChunkClusters * kClusterSize / 64; ++q) {
-                            const int i = q * 64 + lane;
-                            bool can = false;
-                            if (i < P.clusterCount * kClusterSize) {
-                                const DevTri &R = sRec[i];
-                                if (__float_as_int(R.pad0) >= 0) {
-                                    const V3 sv = sub(p0, V3{R.ax, R.ay, R.az});      /* raytracing.c:198 */
-                                    const V3 qv = cross(sv, V3{R.abx, R.aby, R.abz}); /* :202 */
-                                    const float dac = dot(V3{R.acx, R.acy, R.acz}, qv); /* :206 numerator */
-                                    can = dac > 0.f || __float_as_int(R.pad1) == 0;
-                                }
-                            }
-                            reach[q] = __ballot(can);
-                        }
-                        if (lane < P.clusterCount) { /* the cluster's terms and reach mask (bit r: record r) */
-                            const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
-                            const unsigned r8 = (unsigned)((reach[lane >> 3] >> ((lane & 7) * 8)) & 0xffu);
-                            W.cl[lane][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
-                            W.cl[lane][1] = make_float4(t.A, t.B, __uint_as_float(r8), 0.f);
-                        }
-                        wave_lds_sync();
-                    }
-                }
-                if (busy && seg0) {
-                    c = cp;
-                    if (counting && !P.hoist)
-                        tests += L;
-                }
-            }
-            DSECT_END(dq1, 1);
-            if (__any(busy && !seg0)) {
-                unsigned t = 0;
-                const bool useP0 = !MULTI && fromP0 && primKnown && P.clusterCull &&
-                                   fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z) <= kClusterRhoMax;
-                const Closest cb = chain3_trace<MULTI>(P, busy && !seg0, useP0, pos, dir, sRec, W, lane, t);
-                if (busy && !seg0) {
-                    c = cb;
-                    if (counting) {
-                        tests += t;
-                        clTests += (unsigned)P.clusterCount;
-                    }
-                }
-            }
-            /* ---- shading (calcColor, raytracing.c:262-296) ---- */
-            bool endSample = false;
-            DSECT_BEGIN(dq5);
-            if (busy) {
-                if (counting)
-                    calls++;
-                if (c.idx >= 0) {
-                    hits++;
-                    const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
-                    const DevTri &T = P.tris[c.idx];
-                    const DevMat M = P.mats[c.idx];
-                    const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
-                    const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
-                    const V3 specularDir = reflect(dir, normal);
-                    dir = lerp(diffuseDir, specularDir, M.smoothness);
-                    pos = hitPoint;
-                    const V3 emitted = mul(color, M.emission);
-                    light = add(light, mulv(emitted, rayColor));
-                    rayColor = mulv(rayColor, color);
-                    const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-                    endSample = p < random_value(rng);
-                    if (!endSample) {
-                        rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
-                        bounce++;
-                        endSample = bounce >= P.maxBounce;
-                    }
-                    fromP0 = seg0;
-                } else {
-                    light = add(light, mulv(environment(dir, P.env), rayColor)); /* raytracing.c:291 */
-                    endSample = true;
-                }
-                seg0 = false;
-            }
-            DSECT_END(dq5, 5);
-            /* ---- finished samples into the ring (state index myJ) ---- */
-            DSECT_BEGIN(dq7);
-            if (busy && endSample) {
-                const V3 tv = mul(light, P.invSpp); /* calcColor(...) * (float)(1./spp), main.c:99 */
-                const int sl = (int)(myJ & (kRing - 1));
-                W.ring[sl] = make_float4(tv.x, tv.y, tv.z, __int_as_float((int)myJ));
-                W.ringH[sl] = (int)hits;
-                if (counting)
-                    W.ringCnt[sl] = make_uint4(calls, tests, clTests, 0u);
-                busy = false;
-            }
-            wave_lds_sync();
-            /* ---- walk the chain through the finished samples, in sample order (main.c:99) ---- */
-            for (;;) {
-                const int sl = (int)((cj + (unsigned)lane) & (kRing - 1));
-                const float4 e = W.ring[sl];
-                const int eh = W.ringH[sl];
-                const bool valid = __float_as_int(e.w) == (int)(cj + (unsigned)lane);
-                const unsigned long long oneM = __ballot(valid && eh == 1);
-                const int run = oneM == ~0ull ? 64 : (int)__builtin_ctzll(~oneM);
-                const int take = min(run, P.spp - k);
-                uint4 ec = make_uint4(0u, 0u, 0u, 0u);
-                if (counting && valid)
-                    ec = W.ringCnt[sl];
-                if (take > 0) {
-                    if (deferred) {
-                        if (lane < take)
-                            slots[k + lane] = SampleSlot{e.x, e.y, e.z};
-                    } else {
-                        for (int b = 0; b < take; ++b) {
-                            accxy = accxy + f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.x), b)),
-                                               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.y), b))};
-                            accz = accz + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.z), b));
-                        }
-                    }
-                    if (counting && lane < take) {
-                        segCalls += ec.x;
-                        segTraced += P.hoist ? ec.x - 1u : ec.x;
-                        segTests += ec.y;
-                        segClusters += ec.z;
-                    }
-                    k += take;
-                    cj += (unsigned)take;
-                }
-                if (k >= P.spp || take < run)
-                    break;
-                if (run >= 64)
-                    continue; /* 64 one-hit samples consumed: read the next stretch */
-                if (!__builtin_amdgcn_readlane((int)valid, run))
-                    break; /* the chain waits for S_cj */
-                const int hq = __builtin_amdgcn_readlane(eh, run);
-                const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.x), run));
-                const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.y), run));
-                const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.z), run));
-                const int mult = hq == 0 ? P.spp - k : 1; /* a primary miss: every remaining sample is this one */
-                if (deferred) {
-                    for (int kk = k + lane; kk < k + mult; kk += 64)
-                        slots[kk] = SampleSlot{qx, qy, qz};
-                } else {
-                    for (int b = 0; b < mult; ++b) {
-                        accxy = accxy + f2{qx, qy};
-                        accz = accz + qz;
-                    }
-                }
-                if (counting) {
-                    if (lane == run) {
-                        segCalls += (unsigned)mult * ec.x;
-                        segTraced += (unsigned)mult * (P.hoist ? ec.x - 1u : ec.x);
-                        segTests += (unsigned long long)mult * ec.y;
-                        segClusters += (unsigned)mult * ec.z;
-                    }
-                    /* finished samples the chain skips (state indices cj+1 .. cj+hq-1) were evaluated for nothing */
-                    if (valid && lane > run && lane < run + hq)
-                        segSpec += ec.y;
-                }
-                k += mult;
-                if (hq == 0)
-                    break;
-                cj += (unsigned)hq;
-            }
-            DSECT_END(dq7, 7);
-            /* lanes still evaluating state indices the chain has passed: stop them */
-            if (busy && myJ < cj) {
-                busy = false;
-                if (counting)
-                    segSpec += tests;
-            }
-        }
-        /* leftovers: finished samples beyond the chain and lanes still running were evaluated for nothing */
-        if (counting) {
-            const int sl = (int)((cj + (unsigned)lane) & (kRing - 1));
-            if (__float_as_int(W.ring[sl].w) == (int)(cj + (unsigned)lane))
-                segSpec += W.ringCnt[sl].y;
-            if (busy)
-                segSpec += tests;
-        }
-        wave_lds_sync(); /* the ring and tables are rewritten for the next pixel */
-#ifdef RTC_DIAG
-        dPixels++;
-#endif
-        if (deferred) {
-            if (lane == nFin) {
-                finItem = it;
-                finPix = r * P.width + x;
-            }
-            if (++nFin == 64) {
-                chain3_sum_batch(P, nFin, lane, finItem, finPix);
-                nFin = 0;
-            }
-        } else if (lane == 0) {
-            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(accxy.x);
-            P.colors[3 * o + 1] = float_to_u8(accxy.y);
-            P.colors[3 * o + 2] = float_to_u8(accz);
-            if (P.accum) {
-                P.accum[3 * o] = accxy.x;
-                P.accum[3 * o + 1] = accxy.y;
-                P.accum[3 * o + 2] = accz;
-            }
-        }
-    }
-    DSECT_BEGIN(dq6);
-    if (nFin > 0)
-        chain3_sum_batch(P, nFin, lane, finItem, finPix);
-    DSECT_END(dq6, 6);
-#ifdef RTC_DIAG
-    if (lane < 8)
-        atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
-    /* [8] iterations, [9] busy lanes summed over them, [10] samples assigned, [11] pixels, [12] primary traces */
-    if (lane == 0) {
-        atomicAdd(&g_rtc_sect[8], dIters);
-        atomicAdd(&g_rtc_sect[9], dBusy);
-        atomicAdd(&g_rtc_sect[10], dAssigned);
-        atomicAdd(&g_rtc_sect[11], dPixels);
-        atomicAdd(&g_rtc_sect[12], dPrim);
-    }
-#endif
-    if (counting)
-        flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
-}
-
 
 static EnvParams env_of(const Scene &s)
 {
@@ -2922,12 +2278,6 @@ __host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
 #endif
 #ifndef RTC_CHAIN_PRIMF
 #define RTC_CHAIN_PRIMF 1 /* stage the primary filter records in LDS when the block's budget allows */
-#endif
-#ifndef RTC_CHAIN3
-#define RTC_CHAIN3 0 /* rtc_render_chain3 (streaming state indices) instead of rtc_render_chain (windows) */
-#endif
-#ifndef RTC_CHAIN_STAGE
-#define RTC_CHAIN_STAGE 1 /* stage the primary exact and shading records in LDS too */
 #endif
 extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                                      const RtcRenderDesc *d, void *dColors, float *dAccum,
@@ -3062,7 +2412,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result) */
         if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE)) {
-            const size_t per = (size_t)d->spp * sizeof(SampleSlot);
+            const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
             if (need > s->samplesCap) {
@@ -3074,6 +2424,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 ms->samplesCap = need;
             }
             P.sampleBuf = (SampleSlot *)s->samples;
+            P.itemPix = (int *)(s->samples + cap * (size_t)d->spp * sizeof(SampleSlot));
             P.sampleCap = (int)cap;
         }
     }
@@ -3116,34 +2467,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
-            /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then as many of the
-             * primary filter, primary exact and shading records as keep the block within 4 per CU */
+            /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
+             * filter records when the block stays within 4 per CU */
             const size_t rec = s->chunkCount <= 1 ? (size_t)s->clusterCount * kClusterSize * sizeof(DevTri) : 0;
-            size_t dyn = rec;
-            const size_t stat = RTC_CHAIN3 ? kChain3StaticLds : kChainStaticLds;
-            const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF), px = (size_t)s->triPadded * sizeof(DevPrimX),
-                         sh = (size_t)s->triPadded * sizeof(DevShade);
-            P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && stat + dyn + pf <= kChainLdsBudget;
-            dyn += P.chainPrimF ? pf : 0;
-            P.chainStage = 0;
-            if (!RTC_CHAIN3 && RTC_CHAIN_STAGE && stat + dyn + px <= kChainLdsBudget) {
-                P.chainStage |= 1;
-                dyn += px;
-            }
-            if (!RTC_CHAIN3 && RTC_CHAIN_STAGE && stat + dyn + sh <= kChainLdsBudget) {
-                P.chainStage |= 2;
-                dyn += sh;
-            }
-            if (RTC_CHAIN3) {
-                if (s->chunkCount > 1 && dSegments)
-                    hipLaunchKernelGGL((rtc_render_chain3<true, true>), dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
-                else if (s->chunkCount > 1)
-                    hipLaunchKernelGGL((rtc_render_chain3<true, false>), dim3(kChainWorkers), dim3(kChainBlock), 0, st, P);
-                else if (dSegments)
-                    hipLaunchKernelGGL((rtc_render_chain3<false, true>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-                else
-                    hipLaunchKernelGGL((rtc_render_chain3<false, false>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-            } else if (s->chunkCount > 1) {
+            const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
+            P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kChainLdsBudget;
+            const size_t dyn = rec + (P.chainPrimF ? pf : 0);
+            if (s->chunkCount > 1) {
                 if (dSegments)
                     hipLaunchKernelGGL((rtc_render_chain<true, true>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
                 else
@@ -3156,6 +2486,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             HIP_TRY(hipGetLastError());
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
+            if (P.sampleCap > 0) {
+                const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
+                hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
+                HIP_TRY(hipGetLastError());
+            }
             if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
                 HIP_TRY(hipEventRecord(geoEvent, st));
                 geoRecorded = true;

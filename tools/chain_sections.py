@@ -18,9 +18,7 @@ tris, _ = load_tris(scene_name)
 L = rt.lib()
 L.rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
 out = (C.c_ulonglong * 16)()
-names = (["assign", "primary+tables", "cluster_cull", "scan+entries", "pair_passes", "shading+env", "tail_sums", "ring+walk"]
-         if os.environ.get("RTC_SECTIONS", "chain3") == "chain3" else
-         ["rng_setup", "primary_trace", "hit_shading", "cluster_cull", "pair_build", "pair_passes", "env", "walk"])
+names = ["rng_setup", "primary_trace", "hit_shading", "cluster_cull", "pair_build", "pair_passes", "env", "walk"]
 for hoist in (False, True):
     cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist)
     rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
@@ -29,14 +27,9 @@ for hoist in (False, True):
     L.rtc_diag_sections(out, 1)
     tot = sum(out[i] for i in range(8))
     it, alive, act, win, used = (out[i] for i in range(8, 13))
-    if os.environ.get("RTC_SECTIONS", "chain3") == "chain3":
-        print(json.dumps({"hoist": hoist, "iterations": it, "lane_utilisation": round(alive / max(1, 64 * it), 4),
-                          "samples_assigned": act, "pixels": win, "samples_per_pixel": round(act / max(1, win), 2),
-                          "iterations_per_pixel": round(it / max(1, win), 2), "primary_traces": used}), flush=True)
-    else:
-        print(json.dumps({"hoist": hoist, "iterations": it, "lane_utilisation": round(alive / max(1, 64 * it), 4),
-                          "window_lanes_per_window": round(act / max(1, win), 2), "used_lanes_share": round(used / max(1, act), 4),
-                          "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
+    print(json.dumps({"hoist": hoist, "iterations": it, "lane_utilisation": round(alive / max(1, 64 * it), 4),
+                      "window_lanes_per_window": round(act / max(1, win), 2), "used_lanes_share": round(used / max(1, act), 4),
+                      "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
     print(json.dumps({"hoist": hoist, "render_ms": round(st["render_ms"], 3),
                       "share": {n: round(out[i] / tot, 4) for i, n in enumerate(names)},
                       "cycles": {n: int(out[i]) for i, n in enumerate(names)}}), flush=True)

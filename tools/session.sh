@@ -13,11 +13,13 @@ step() {  # step <name> <timeout> <cmd...>
   return $rc
 }
 step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
-for w in ultracomplex_1080p64 fsuzane_1080p64 ultracomplex_4k64; do
-  for lib in librtc_chainold.so librtc.so librtc_nostage.so librtc_chain3.so; do
+for w in ultracomplex_1080p64 ultracomplex_4k64 fsuzane_1080p64; do
+  for lib in librtc.so librtc_waves5.so librtc_waves5s.so; do
     RTC_LIB_PATH=$R/raytracingc_amd/_lib/$lib step "ab_${w}_${lib%.so}" 150 python bench.py --workload $w --steps 30 --warmup 5 --no-cpu-baseline --no-extras || exit $?
   done
 done
-RTC_SECTIONS=chain2 step sec_ultracomplex 120 python tools/chain_sections.py ultracomplex || exit $?
-RTC_SECTIONS=chain2 step sec_fsuzane 120 python tools/chain_sections.py fsuzane || exit $?
+step scale1080 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
+cd /tmp
+step loop8 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop8" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 60 overlap 8 || exit $?
+step loop1 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
 echo done
