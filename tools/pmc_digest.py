@@ -35,7 +35,8 @@ stats = {}
 for f in glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = short(r["Name"])
-        if k:
+        # the timed instantiation: rtc_render_chain<MULTI, COUNT=false>; the counting one runs only for the counters
+        if k and not r["Name"].endswith("true>(RenderParams)"):
             stats[k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                         "total_ms": float(r["TotalDurationNs"]) / 1e6}
 # counters: every pass directory pmc_* holds one counter group over the same renders
@@ -45,7 +46,7 @@ for d in sorted(glob.glob(os.path.join(root, "pmc_*"))):
         acc = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
             k = short(r.get("Kernel_Name", ""))
-            if k:
+            if k and not r.get("Kernel_Name", "").endswith("true>(RenderParams)"):
                 acc[k][(r["Counter_Name"], r.get("Dispatch_Id"))] += float(r["Counter_Value"])
         for k, cv in acc.items():
             by = collections.defaultdict(list)

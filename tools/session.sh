@@ -12,14 +12,11 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
-for w in ultracomplex_1080p64 ultracomplex_4k64 fsuzane_1080p64; do
-  for lib in librtc.so librtc_waves5.so librtc_waves5s.so; do
-    RTC_LIB_PATH=$R/raytracingc_amd/_lib/$lib step "ab_${w}_${lib%.so}" 150 python bench.py --workload $w --steps 30 --warmup 5 --no-cpu-baseline --no-extras || exit $?
-  done
-done
-step scale1080 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
-cd /tmp
-step loop8 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop8" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 60 overlap 8 || exit $?
-step loop1 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
+tag=${1:-r03_c}
+step pytest_$tag 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
+step smoke_$tag 200 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step bench_$tag 400 python bench.py || exit $?
+step scale1080_$tag 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
+step scale4k_$tag 200 python tools/scale_probe.py 5 3840 2160 64 overlap || exit $?
+bash tools/profile_workload.sh ultracomplex_1080p64 $tag || exit $?
 echo done
