@@ -179,7 +179,8 @@ static __device__ __forceinline__ void random_normals_exact(unsigned &s, float v
  * path (rtc_math.h bm_rho_fast / bm_normal_fast: table-driven log and cos, each float returned only when it
  * provably rounds like the reference's); a lane with any uncertified value (~4e-6 per normal) redraws all three
  * from the saved state with the exact restatement (random_normal). */
-__device__ __forceinline__ V3 random_direction(unsigned &s)
+__device__ __forceinline__ V3 random_direction(unsigned &s, const rtcmath::BmLogEntry *logTab = rtcmath::kBmLogTab,
+                                              const double (*cosTab)[2] = rtcmath::kBmCosTab)
 {
 #ifndef RTC_EXACT_BM
     const unsigned s0 = s;
@@ -193,8 +194,8 @@ __device__ __forceinline__ V3 random_direction(unsigned &s)
     for (int c = 0; c < 3; ++c) {
         const float theta = (float)(2 * 3.14159265 * (double)random_value(s)); /* moremath.c:99 */
         float rho;
-        ok = rtcmath::bm_rho_fast(random_value(s), rho) && ok;
-        ok = rtcmath::bm_normal_fast(rho, theta, v[c]) && ok;
+        ok = rtcmath::bm_rho_fast(random_value(s), rho, logTab) && ok;
+        ok = rtcmath::bm_normal_fast(rho, theta, v[c], cosTab) && ok;
     }
     if (__builtin_expect(!ok, 0)) {
         s = s0;

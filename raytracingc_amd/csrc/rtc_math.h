@@ -432,11 +432,11 @@ constexpr double kBmNrmTol = 0x1p-46; /* absolute, per unit rho */
 RTC_HD double bm_half_ulp(float f) { return u2d((unsigned long long)(((f2u(f) >> 23) & 0xffu) + 1023u - 151u) << 52); }
 
 /* sqrt(-2 log((double)u)) in double, for u in (0, 1] (the fast scheme, before certification) */
-RTC_HD double bm_rho_d(float u)
+RTC_HD double bm_rho_d(float u, const BmLogEntry *logTab = kBmLogTab)
 {
     const unsigned iu = f2u(u);
     const unsigned tmp = iu - 0x3f330000u;
-    const BmLogEntry e = kBmLogTab[(tmp >> 16) & 127u];
+    const BmLogEntry e = logTab[(tmp >> 16) & 127u];
     const double dk = (double)((int)tmp >> 23);
     const double r = fma((double)u2f(iu - (tmp & 0xff800000u)), (double)e.invc, -1.0); /* exact */
     double q = 1.0 / 7.0; /* log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6 + r^5/7) */
@@ -451,16 +451,16 @@ RTC_HD double bm_rho_d(float u)
     return __builtin_sqrt(-2.0 * (hi + lo));
 }
 /* rho = (float)sqrt(-2 log((double)u)) for u in (0, 1]; false: not certified (use the exact path) */
-RTC_HD bool bm_rho_fast(float u, float &rho)
+RTC_HD bool bm_rho_fast(float u, float &rho, const BmLogEntry *logTab = kBmLogTab)
 {
-    const double rd = bm_rho_d(u);
+    const double rd = bm_rho_d(u, logTab);
     const float f = (float)rd;
     rho = f;
     const double d = fabs(rd - (double)f);
     return (f2u(f) & 0x7f800000u) != 0u && f2u(u) >= 0x00800000u && d < fma(-rd, kBmRhoTol, bm_half_ulp(f));
 }
 /* cos((double)theta) in double for theta in [0, 2 pi] (the fast scheme) */
-RTC_HD double bm_cos_d(float theta)
+RTC_HD double bm_cos_d(float theta, const double (*cosTab)[2] = kBmCosTab)
 {
     const double th = (double)theta;
     const double jd = rint(th * kBmInvStep);
@@ -478,12 +478,12 @@ RTC_HD double bm_cos_d(float theta)
     sn = fma(sn, z, -1.0 / 6.0);
     sn = fma(sn * z, t, t);
     const int j = (int)jd & 63;
-    return fma(kBmCosTab[j][0], c, -kBmCosTab[j][1] * sn);
+    return fma(cosTab[j][0], c, -cosTab[j][1] * sn);
 }
 /* n = (float)((double)rho * cos((double)theta)) for theta = (float)(2 pi u) in [0, 2 pi]; false: not certified */
-RTC_HD bool bm_normal_fast(float rho, float theta, float &n)
+RTC_HD bool bm_normal_fast(float rho, float theta, float &n, const double (*cosTab)[2] = kBmCosTab)
 {
-    const double rd = (double)rho * bm_cos_d(theta);
+    const double rd = (double)rho * bm_cos_d(theta, cosTab);
     const float f = (float)rd;
     n = f;
     const double d = fabs(rd - (double)f);

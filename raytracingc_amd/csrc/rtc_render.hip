@@ -1309,7 +1309,7 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 /* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
 __device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
-__shared__ unsigned long long s_rtc_sect[16][8];
+__shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..15 (rtc_render_chain) */
 #define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define DSECT_END(v, k)                                                                                        \
     do {                                                                                                       \
@@ -1711,6 +1711,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef RTC_CHAIN_PAIRS
 #define RTC_CHAIN_PAIRS 1024
 #endif
+#ifndef RTC_BM_LDS
+#define RTC_BM_LDS 1 /* rtc_render_chain: the Box-Muller tables in LDS */
+#endif
 struct ChainWaveLds {
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
@@ -1724,7 +1727,8 @@ static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
-constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
+                                   (RTC_BM_LDS ? 128 * sizeof(rtcmath::BmLogEntry) + 64 * 16 : 0);
 #ifndef RTC_CHAIN_WGS_PER_CU
 #define RTC_CHAIN_WGS_PER_CU 4
 #endif
@@ -1781,7 +1785,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     const bool rhoOk = P.clusterCull && rho <= kClusterRhoMax;
     tests = 0;
     /* A pixel's first bounces all start at its primary hit point p0 (lane 0's pos; single-chunk scenes):
-     *  - the clusters' origin terms, once, one lane per cluster, into LDS;
+     *  - the clusters' origin terms, once, one lane per cluster, into LDS, compacted to the clusters with a
+     *    record reachable from p0 (below), so the per-lane cull loop is branch-free over those only;
      *  - the records that can be hit from p0 at all, one lane per record: the reference's own f32
      *    dot(AC, (p0 - A) x AB) > 0, or a stored normal not aligned with the geometric one (aligned_normal:
      *    with an aligned normal and that dot <= 0, rayTriangle rejects every direction from p0).
@@ -1789,15 +1794,12 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
      * holds for |dir|_1 <= kClusterRhoMax: a wave with a live ray beyond that takes the per-cluster path. */
     const bool table = !MULTI && firstBounce && P.clusterCull && !__ballot(alive && !rhoOk);
     unsigned long long reach[kChunkClusters * kClusterSize / 64];
+    unsigned long long live = 0; /* clusters with a record reachable from p0 (their terms compacted in W.cl) */
+    DSECT_BEGIN(dtab);
     if (table) {
         const V3 p0{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.x), 0)),
                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.y), 0)),
                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.z), 0))};
-        if (lane < P.clusterCount) {
-            const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
-            W.cl[lane][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
-            W.cl[lane][1] = make_float4(t.A, t.B, 0.f, 0.f);
-        }
 #pragma unroll
         for (int q = 0; q < kChunkClusters * kClusterSize / 64; ++q) {
             const int i = q * 64 + lane;
@@ -1813,8 +1815,24 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
             }
             reach[q] = __ballot(can);
         }
+        /* lane k < clusterCount: cluster k's reachable records r8; the clusters with any enter W.cl compacted, in
+         * cluster order, with (k, r8) in the second vector */
+        unsigned r8l = 0;
+        if (lane < P.clusterCount) {
+            const unsigned long long rw = lane < 8 ? reach[0] : lane < 16 ? reach[1] : lane < 24 ? reach[2] : reach[3];
+            r8l = (unsigned)(rw >> ((lane & 7) * 8)) & 0xffu;
+        }
+        live = __ballot(r8l != 0u);
+        if (r8l) {
+            const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(live >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)live, 0u));
+            const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
+            W.cl[pos][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
+            W.cl[pos][1] = make_float4(t.A, t.B, __int_as_float(lane), __int_as_float((int)r8l));
+        }
         wave_lds_sync();
     }
+    DSECT_END(dtab, 14);
     /* scenes of more than kChunkClusters clusters: chunk by chunk (a chunk's ball culls its clusters for a lane
      * at once); the records come from global memory when they are not staged in LDS (sRec null) */
     const int nChunks = MULTI ? P.chunkCount : 1;
@@ -1829,17 +1847,16 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         }
         unsigned cm = 0;
         DSECT_BEGIN(dc3);
+        /* table mode: bit j of cm = the j-th live cluster kept (branch-free body over the compacted terms) */
+        const int nLive = __popcll(live);
         if (in && table) {
-            for (int k = 0; k < nCl; ++k) {
-                const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
-                if (!r8)
-                    continue; /* no record of the cluster can be hit from p0 */
-                const float4 a = W.cl[k][0], b = W.cl[k][1];
+#pragma unroll 4
+            for (int j = 0; j < nLive; ++j) {
+                const float4 a = W.cl[j][0], b = W.cl[j][1];
                 const ClusterTerms t{V3{a.x, a.y, a.z}, a.w, b.x, b.y};
-                if (!(rhoOk && culled_by(t, dir, rho, dd))) {
-                    cm |= 1u << k;
-                    tests += (unsigned)__popc(r8);
-                }
+                const bool kept = !(rhoOk && culled_by(t, dir, rho, dd));
+                cm |= (unsigned)kept << j;
+                tests += kept ? (unsigned)__popc((unsigned)__float_as_int(b.w)) : 0u;
             }
         } else if (in) {
             for (int k = 0; k < nCl; ++k)
@@ -1856,9 +1873,11 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         if (table) {
             /* (lane, record) entries for the reachable records of the clusters each lane kept; the list is
              * flushed through the passes whenever the next cluster would overflow it */
-            for (int k = 0; k < nCl; ++k) {
+            unsigned long long lv = live;
+            for (int j = 0; lv; ++j, lv &= lv - 1) {
+                const int k = __builtin_ctzll(lv); /* the j-th live cluster */
                 const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
-                const unsigned long long m = __ballot((cm >> k) & 1u);
+                const unsigned long long m = __ballot((cm >> j) & 1u);
                 if (!m)
                     continue;
                 const int per = __popc(r8), cnt = (int)__popcll(m) * per;
@@ -1868,7 +1887,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                     wave_lds_sync();
                     n = 0;
                 }
-                if ((cm >> k) & 1u) {
+                if ((cm >> j) & 1u) {
                     int e = n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) * per;
                     for (unsigned r = r8; r; r &= r - 1)
@@ -2012,15 +2031,30 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
+#if RTC_BM_LDS
+    /* the certified Box-Muller tables (rtc_bm_tables.h), read at lane-varying indices at every hit */
+    __shared__ rtcmath::BmLogEntry sBmLog[128];
+    __shared__ double sBmCos[64][2];
+    for (int i = threadIdx.x; i < 128; i += kChainBlock)
+        sBmLog[i] = rtcmath::kBmLogTab[i];
+    for (int i = threadIdx.x; i < 64; i += kChainBlock) {
+        sBmCos[i][0] = rtcmath::kBmCosTab[i][0];
+        sBmCos[i][1] = rtcmath::kBmCosTab[i][1];
+    }
+#define RTC_BM_TABS , sBmLog, sBmCos
+#else
+#define RTC_BM_TABS
+#endif
     if (threadIdx.x == 0)
         sWork = 0;
     sPow.fill(threadIdx.x);
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
     const DevTri *sRec = S.rec;
 #ifdef RTC_DIAG
-    if ((threadIdx.x & 63) < 8)
+    if ((threadIdx.x & 63) < 16)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
 #endif
+    DSECT_BEGIN(dtot);
     __syncthreads();
     sPow.attach(P.env);
     const int lane = threadIdx.x & 63;
@@ -2043,6 +2077,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
     for (;;) {
+        DSECT_BEGIN(dset);
         const int it = __builtin_amdgcn_readfirstlane(nextIt);
         while (it - base >= cnt && l < kGeoLists - 1) {
             base += cnt;
@@ -2073,6 +2108,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 segTests += L;
             }
         }
+        DSECT_END(dset, 15);
         f2 accxy{0.f, 0.f}; /* the pixel's accumulator (main.c:97): x, y packed, z */
         float accz = 0.f;
         int k = 0;       /* samples accumulated */
@@ -2134,7 +2170,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         const DevTri &T = P.tris[c.idx];
                         const DevMat M = P.mats[c.idx];
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
-                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng RTC_BM_TABS)));
                         const V3 specularDir = reflect(dir, normal);
                         dir = lerp(diffuseDir, specularDir, M.smoothness);
                         pos = hitPoint;
@@ -2242,7 +2278,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
     }
 #ifdef RTC_DIAG
-    if (lane < 8)
+    DSECT_END(dtot, 13);
+    if (lane < 8 || (lane >= 13 && lane < 16))
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
     /* [8] bounce-loop iterations, [9] live lanes summed over them, [10] window lanes, [11] windows, [12] lanes
      * whose sample was used */

@@ -32,4 +32,8 @@ for hoist in (False, True):
                       "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
     print(json.dumps({"hoist": hoist, "render_ms": round(st["render_ms"], 3),
                       "share": {n: round(out[i] / tot, 4) for i, n in enumerate(names)},
-                      "cycles": {n: int(out[i]) for i, n in enumerate(names)}}), flush=True)
+                      "cycles": {n: int(out[i]) for i, n in enumerate(names)},
+                      # 13: whole wave lifetime, 14: first-bounce tables (cluster terms, reach), 15: item fetch and
+                      # pixel setup -- the sections above cover tot / lifetime of the waves' cycles
+                      "wave_cycles": int(out[13]), "table_build": int(out[14]), "item_setup": int(out[15]),
+                      "covered": round((tot + out[14] + out[15]) / max(1, out[13]), 4)}), flush=True)

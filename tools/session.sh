@@ -12,11 +12,9 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-tag=${1:-r03_c}
-step pytest_$tag 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
-step smoke_$tag 200 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-step bench_$tag 400 python bench.py || exit $?
-step scale1080_$tag 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
-step scale4k_$tag 200 python tools/scale_probe.py 5 3840 2160 64 overlap || exit $?
-bash tools/profile_workload.sh ultracomplex_1080p64 $tag || exit $?
+step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
+step ab 600 bash tools/ab_bench_libs.sh librtc.so librtc_w512.so librtc_w256.so || exit $?
+for l in librtc librtc_w512 librtc_w256; do
+  RTC_LIB_PATH=$R/raytracingc_amd/_lib/$l.so step scale_$l 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
+done
 echo done
