@@ -1708,8 +1708,40 @@ constexpr int kChainWorkers = RTC_CHAIN_WORKERS;
  * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
 typedef float f2 __attribute__((ext_vector_type(2)));
+/* Data this kernel only reads (written by earlier kernels of the launch) at a wave-uniform address, read through
+ * the constant address space so that the compiler issues scalar loads (RTC_CHAIN_SMEM): they return on lgkmcnt,
+ * so waiting for one does not also wait for the wave's earlier sample-slot stores to be acknowledged, as a
+ * vector load's vmcnt wait does on gfx9 (loads and stores share vmcnt). */
+#ifndef RTC_CHAIN_SMEM
+#define RTC_CHAIN_SMEM 1
+#endif
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *kconst(const T *p)
+{
+    return (const __attribute__((address_space(4))) T *)p;
+}
+/* a record of T (a multiple of 4 bytes) from a wave-uniform address, dword by dword through kconst */
+template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
+{
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    T v;
+    const __attribute__((address_space(4))) unsigned *q = kconst((const unsigned *)(p + i));
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k)
+        ((unsigned *)&v)[k] = q[k];
+    return v;
+}
+#if RTC_CHAIN_SMEM
+#define KCONST(p) kconst(p)
+#define KLOAD(p, i) kload(p, i)
+#else
+#define KCONST(p) (p)
+#define KLOAD(p, i) ((p)[i])
+#endif
 #ifndef RTC_CHAIN_PAIRS
 #define RTC_CHAIN_PAIRS 1024
+#endif
+#ifndef RTC_TABLE_CL
+#define RTC_TABLE_CL 1 /* first-bounce pairs per (lane, cluster) instead of per (lane, record) */
 #endif
 #ifndef RTC_BM_LDS
 #define RTC_BM_LDS 1 /* rtc_render_chain: the Box-Muller tables in LDS */
@@ -1768,6 +1800,33 @@ __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, 
                     surv &= surv - 1;
                     general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
                 }
+            }
+            if (c.idx >= 0 && c.dst < 999999.f)
+                atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
+        }
+    }
+}
+
+/* RTC_TABLE_CL: the first-bounce pairs as (lane, live cluster j) -- one entry per cluster a lane keeps, the pass
+ * looping over that cluster's records reachable from p0 (W.cl[j][1]: z = cluster index, w = reach bits); one
+ * atomic per entry instead of one per record */
+__device__ __forceinline__ void chain_pair_passes_cl(int n, const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
+                                                     V3 pos, V3 dir)
+{
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        const unsigned pr = i < n ? W.pair[i] : (unsigned)lane;
+        const int o = (int)(pr & 63u);
+        const V3 rpos{bperm_f(o, pos.x), bperm_f(o, pos.y), bperm_f(o, pos.z)};
+        const V3 rdir{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
+        if (i < n) {
+            const float4 kb = W.cl[pr >> 6][1];
+            const DevTri *R = sRec + __float_as_int(kb.z) * kClusterSize;
+            Closest c{999999.f, -1};
+            for (unsigned r = (unsigned)__float_as_int(kb.w); r; r &= r - 1) {
+                const DevTri &T = R[__builtin_ctz(r)];
+                if (general_filter(rpos, rdir, T))
+                    general_exact(rpos, rdir, T, __float_as_int(T.pad0), c);
             }
             if (c.idx >= 0 && c.dst < 999999.f)
                 atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
@@ -1870,7 +1929,24 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_BEGIN(dc4);
         int n = 0;
         constexpr int kCap = RTC_CHAIN_PAIRS;
-        if (table) {
+        if (table && RTC_TABLE_CL) {
+            for (int j = 0; j < nLive; ++j) {
+                const unsigned long long m = __ballot((cm >> j) & 1u);
+                if (!m)
+                    continue;
+                if (n + (int)__popcll(m) > kCap) {
+                    wave_lds_sync();
+                    chain_pair_passes_cl(n, sRec, W, lane, pos, dir);
+                    wave_lds_sync();
+                    n = 0;
+                }
+                if ((cm >> j) & 1u)
+                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                        (unsigned short)(lane | (j << 6));
+                n += (int)__popcll(m);
+            }
+        } else if (table) {
             /* (lane, record) entries for the reachable records of the clusters each lane kept; the list is
              * flushed through the passes whenever the next cluster would overflow it */
             unsigned long long lv = live;
@@ -1916,7 +1992,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         wave_lds_sync();
         DSECT_END(dc4, 4);
         DSECT_BEGIN(dc5);
-        if (table)
+        if (table && RTC_TABLE_CL)
+            chain_pair_passes_cl(n, sRec, W, lane, pos, dir);
+        else if (table)
             chain_pair_passes<MULTI, true>(P, n, c0, sRec, W, lane, pos, dir);
         else
             chain_pair_passes<MULTI, false>(P, n, c0, sRec, W, lane, pos, dir);
@@ -1975,14 +2053,14 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
                                                            const DevPrimF *__restrict__ sF)
 {
     for (int w = 0; w < P.maskWords; ++w) {
-        unsigned long long m = mask[w];
+        unsigned long long m = KCONST(mask)[w];
         while (m) {
             const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
             const DevPrimF F = sF ? sF[t] : P.primF[t];
             if (!prim_backfacing(dir, F) && prim_pass(dir, F) && !(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
                 /* the reference's arithmetic (raytracing.c:189-208) */
-                const DevPrimX X = P.primX[t];
+                const DevPrimX X = KLOAD(P.primX, t);
                 const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
                 const float det = dot(V3{X.abx, X.aby, X.abz}, h);
                 if (!(-kEps < det && det < kEps)) {
@@ -2075,20 +2153,20 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #ifdef RTC_DIAG
     unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
 #endif
-    int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(P.geoCount[0]);
+    int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(KCONST(P.geoCount)[0]);
     for (;;) {
         DSECT_BEGIN(dset);
         const int it = __builtin_amdgcn_readfirstlane(nextIt);
         while (it - base >= cnt && l < kGeoLists - 1) {
             base += cnt;
             ++l;
-            cnt = __builtin_amdgcn_readfirstlane(P.geoCount[l * kGeoCountStride]);
+            cnt = __builtin_amdgcn_readfirstlane(KCONST(P.geoCount)[l * kGeoCountStride]);
         }
         if (it - base >= cnt)
             break;
         if (lane == 0)
             nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
-        const int code = __builtin_amdgcn_readfirstlane(P.geoList[(size_t)l * P.geoCap + (it - base)]);
+        const int code = __builtin_amdgcn_readfirstlane(KCONST(P.geoList)[(size_t)l * P.geoCap + (it - base)]);
         const int tile = code >> 6, bit = code & 63;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
         const int y = P.rowStart + r * P.rowStride;
@@ -2167,8 +2245,16 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         hits++;
                         /* calcColor hit branch, raytracing.c:272-287 */
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
-                        const DevTri &T = P.tris[c.idx];
-                        const DevMat M = P.mats[c.idx];
+                        DevTri T;
+                        DevMat M;
+                        if (RTC_CHAIN_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
+                            const int u = __builtin_amdgcn_readfirstlane(c.idx);
+                            T = KLOAD(P.tris, u);
+                            M = KLOAD(P.mats, u);
+                        } else {
+                            T = P.tris[c.idx];
+                            M = P.mats[c.idx];
+                        }
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
                         const V3 diffuseDir = normalized(add(normal, random_direction(rng RTC_BM_TABS)));
                         const V3 specularDir = reflect(dir, normal);

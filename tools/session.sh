@@ -13,8 +13,8 @@ step() {  # step <name> <timeout> <cmd...>
   return $rc
 }
 step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
-step ab 600 bash tools/ab_bench_libs.sh librtc.so librtc_w512.so librtc_w256.so || exit $?
-for l in librtc librtc_w512 librtc_w256; do
-  RTC_LIB_PATH=$R/raytracingc_amd/_lib/$l.so step scale_$l 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
-done
+step ab 900 bash tools/ab_bench_libs.sh librtc.so librtc_smem0.so || exit $?
+step sections 200 python tools/chain_sections.py || exit $?
+
+cd /tmp
 echo done
