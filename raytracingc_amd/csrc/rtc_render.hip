@@ -588,6 +588,36 @@ struct RenderParams {
     EnvParams env;
 };
 
+/* Data a kernel only reads (written by earlier kernels of the launch) at a wave-uniform address, read through
+ * the constant address space so that the compiler issues scalar loads (RTC_SMEM): they return on lgkmcnt,
+ * so waiting for one does not also wait for the wave's earlier sample-slot stores to be acknowledged, as a
+ * vector load's vmcnt wait does on gfx9 (loads and stores share vmcnt). */
+#ifndef RTC_SMEM
+#define RTC_SMEM 1
+#endif
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *kconst(const T *p)
+{
+    return (const __attribute__((address_space(4))) T *)p;
+}
+/* a record of T (a multiple of 4 bytes) from a wave-uniform address, dword by dword through kconst */
+template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
+{
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    T v;
+    const __attribute__((address_space(4))) unsigned *q = kconst((const unsigned *)(p + i));
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k)
+        ((unsigned *)&v)[k] = q[k];
+    return v;
+}
+#if RTC_SMEM
+#define KCONST(p) kconst(p)
+#define KLOAD(p, i) kload(p, i)
+#else
+#define KCONST(p) (p)
+#define KLOAD(p, i) ((p)[i])
+#endif
+
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 constexpr int kGeoLists = 16, kGeoCountStride = 32; /* ints: one 128-B line per counter */
 
@@ -1178,7 +1208,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const DevPrimF F = P.primF[w * 64 + j];
+            const DevPrimF F = KLOAD(P.primF, w * 64 + j);
             const bool keep = (int)px.valid & (int)!prim_backfacing(px.dir, F) & (int)prim_pass(px.dir, F);
             anyCand |= keep;
             if (__ballot(keep))
@@ -1708,35 +1738,6 @@ constexpr int kChainWorkers = RTC_CHAIN_WORKERS;
  * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
 typedef float f2 __attribute__((ext_vector_type(2)));
-/* Data this kernel only reads (written by earlier kernels of the launch) at a wave-uniform address, read through
- * the constant address space so that the compiler issues scalar loads (RTC_CHAIN_SMEM): they return on lgkmcnt,
- * so waiting for one does not also wait for the wave's earlier sample-slot stores to be acknowledged, as a
- * vector load's vmcnt wait does on gfx9 (loads and stores share vmcnt). */
-#ifndef RTC_CHAIN_SMEM
-#define RTC_CHAIN_SMEM 1
-#endif
-template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *kconst(const T *p)
-{
-    return (const __attribute__((address_space(4))) T *)p;
-}
-/* a record of T (a multiple of 4 bytes) from a wave-uniform address, dword by dword through kconst */
-template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
-{
-    static_assert(sizeof(T) % 4 == 0, "dword records");
-    T v;
-    const __attribute__((address_space(4))) unsigned *q = kconst((const unsigned *)(p + i));
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(T) / 4); ++k)
-        ((unsigned *)&v)[k] = q[k];
-    return v;
-}
-#if RTC_CHAIN_SMEM
-#define KCONST(p) kconst(p)
-#define KLOAD(p, i) kload(p, i)
-#else
-#define KCONST(p) (p)
-#define KLOAD(p, i) ((p)[i])
-#endif
 #ifndef RTC_CHAIN_PAIRS
 #define RTC_CHAIN_PAIRS 1024
 #endif
@@ -2050,14 +2051,16 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
  * (survivors only) stays global.  Same operations as closest_primary_listed. */
 __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P, V3 dir, Closest &c,
                                                            const unsigned long long *__restrict__ mask,
-                                                           const DevPrimF *__restrict__ sF)
+                                                           const DevPrimF *__restrict__ sF, bool staged)
 {
     for (int w = 0; w < P.maskWords; ++w) {
         unsigned long long m = KCONST(mask)[w];
         while (m) {
             const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            const DevPrimF F = sF ? sF[t] : P.primF[t];
+            /* two loads of known address space (LDS, or a scalar load): a pointer that may be either would be
+             * read with flat loads, whose wait also covers the wave's pending slot stores */
+            const DevPrimF F = staged ? sF[t] : KLOAD(P.primF, t);
             if (!prim_backfacing(dir, F) && prim_pass(dir, F) && !(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
                 /* the reference's arithmetic (raytracing.c:189-208) */
                 const DevPrimX X = KLOAD(P.primX, t);
@@ -2128,6 +2131,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     sPow.fill(threadIdx.x);
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
     const DevTri *sRec = S.rec;
+    /* the staged primary filter records: always the LDS address (never null), used when P.chainPrimF */
+    const DevPrimF *sPF = (const DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
+    const bool pfStaged = P.chainPrimF != 0;
 #ifdef RTC_DIAG
     if ((threadIdx.x & 63) < 16)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
@@ -2180,7 +2186,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            closest_primary_listed_lds(P, pdir, prim, mask, S.primF);
+            closest_primary_listed_lds(P, pdir, prim, mask, sPF, pfStaged);
             if (counting && lane == 0) {
                 segTraced++;
                 segTests += L;
@@ -2222,7 +2228,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            closest_primary_listed_lds(P, dir, c, mask, S.primF);
+                            closest_primary_listed_lds(P, dir, c, mask, sPF, pfStaged);
                             if (counting)
                                 tests += L;
                         }
@@ -2247,7 +2253,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
                         DevTri T;
                         DevMat M;
-                        if (RTC_CHAIN_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
+                        if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
                             const int u = __builtin_amdgcn_readfirstlane(c.idx);
                             T = KLOAD(P.tris, u);
                             M = KLOAD(P.mats, u);

@@ -15,6 +15,6 @@ step() {  # step <name> <timeout> <cmd...>
 step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
 step ab 900 bash tools/ab_bench_libs.sh librtc.so librtc_smem0.so || exit $?
 step sections 200 python tools/chain_sections.py || exit $?
-
 cd /tmp
+step loop1 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
 echo done
