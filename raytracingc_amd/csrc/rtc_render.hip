@@ -1745,7 +1745,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define RTC_TABLE_CL 1 /* first-bounce pairs per (lane, cluster) instead of per (lane, record) */
 #endif
 #ifndef RTC_BM_LDS
-#define RTC_BM_LDS 1 /* rtc_render_chain: the Box-Muller tables in LDS */
+#define RTC_BM_LDS 0 /* rtc_render_chain: the Box-Muller tables in LDS */
 #endif
 struct ChainWaveLds {
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */

@@ -3,7 +3,7 @@
 set -u
 wl=ultracomplex_1080p64
 if [ "${1:-}" = "--workload" ]; then wl=$2; shift 2; fi
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for l in "$@"; do
     RTC_LIB_PATH=$GRAFT_REPO_ROOT/raytracingc_amd/_lib/$l timeout -k 10 200 python bench.py --workload $wl --steps 50 --warmup 5 \
       --no-extras --no-cpu-baseline > gpurun_out/abl.log 2>&1 || { echo "$l failed"; exit 1; }
