@@ -1741,12 +1741,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef RTC_CHAIN_PAIRS
 #define RTC_CHAIN_PAIRS 1024
 #endif
-#ifndef RTC_TABLE_CL
-#define RTC_TABLE_CL 1 /* first-bounce pairs per (lane, cluster) instead of per (lane, record) */
-#endif
-#ifndef RTC_BM_LDS
-#define RTC_BM_LDS 0 /* rtc_render_chain: the Box-Muller tables in LDS */
-#endif
 struct ChainWaveLds {
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
@@ -1760,21 +1754,20 @@ static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
-constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
-                                   (RTC_BM_LDS ? 128 * sizeof(rtcmath::BmLogEntry) + 64 * 16 : 0);
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
 #ifndef RTC_CHAIN_WGS_PER_CU
 #define RTC_CHAIN_WGS_PER_CU 4
 #endif
 constexpr size_t kChainLdsBudget = 160 * 1024 / RTC_CHAIN_WGS_PER_CU;
 
-/* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records -- or, with
- * ONE, a (lane, record) pair; the owner's ray by ds_bpermute from the owner lane (every lane takes part), the
- * exact-safe filter, the reference arithmetic for survivors, an atomic lexicographic minimum into the owner's key. */
+/* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records; the owner's ray
+ * by ds_bpermute from the owner lane (every lane takes part), the exact-safe filter, the reference arithmetic for
+ * survivors, an atomic lexicographic minimum into the owner's key. */
 __device__ __forceinline__ float bperm_f(int srcLane, float v)
 {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane << 2, __float_as_int(v)));
 }
-template <bool MULTI, bool ONE>
+template <bool MULTI>
 __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, int c0, const DevTri *__restrict__ sRec,
                                                   ChainWaveLds &W, int lane, V3 pos, V3 dir)
 {
@@ -1786,29 +1779,22 @@ __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, 
         const V3 rdir{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
         if (i < n) {
             Closest c{999999.f, -1};
-            if (ONE) {
-                const DevTri &R = sRec[pr >> 6];
-                if (general_filter(rpos, rdir, R))
-                    general_exact(rpos, rdir, R, __float_as_int(R.pad0), c);
-            } else {
-                const DevTri *R = (MULTI ? P.clTris : sRec) + (c0 + (int)(pr >> 6)) * kClusterSize;
-                unsigned surv = 0;
+            const DevTri *R = (MULTI ? P.clTris : sRec) + (c0 + (int)(pr >> 6)) * kClusterSize;
+            unsigned surv = 0;
 #pragma unroll RTC_CHAIN_UNROLL
-                for (int j = 0; j < kClusterSize; ++j)
-                    surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
-                while (surv) {
-                    const int j = __builtin_ctz(surv);
-                    surv &= surv - 1;
-                    general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
-                }
+            for (int j = 0; j < kClusterSize; ++j)
+                surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
+            while (surv) {
+                const int j = __builtin_ctz(surv);
+                surv &= surv - 1;
+                general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
             }
             if (c.idx >= 0 && c.dst < 999999.f)
                 atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
         }
     }
 }
-
-/* RTC_TABLE_CL: the first-bounce pairs as (lane, live cluster j) -- one entry per cluster a lane keeps, the pass
+/* The first-bounce pairs as (lane, live cluster j) -- one entry per cluster a lane keeps, the pass
  * looping over that cluster's records reachable from p0 (W.cl[j][1]: z = cluster index, w = reach bits); one
  * atomic per entry instead of one per record */
 __device__ __forceinline__ void chain_pair_passes_cl(int n, const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
@@ -1930,7 +1916,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_BEGIN(dc4);
         int n = 0;
         constexpr int kCap = RTC_CHAIN_PAIRS;
-        if (table && RTC_TABLE_CL) {
+        if (table) {
+            /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
+             * whenever the next cluster would overflow it */
             for (int j = 0; j < nLive; ++j) {
                 const unsigned long long m = __ballot((cm >> j) & 1u);
                 if (!m)
@@ -1947,31 +1935,6 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                         (unsigned short)(lane | (j << 6));
                 n += (int)__popcll(m);
             }
-        } else if (table) {
-            /* (lane, record) entries for the reachable records of the clusters each lane kept; the list is
-             * flushed through the passes whenever the next cluster would overflow it */
-            unsigned long long lv = live;
-            for (int j = 0; lv; ++j, lv &= lv - 1) {
-                const int k = __builtin_ctzll(lv); /* the j-th live cluster */
-                const unsigned r8 = (unsigned)(reach[k >> 3] >> ((k & 7) * 8)) & 0xffu;
-                const unsigned long long m = __ballot((cm >> j) & 1u);
-                if (!m)
-                    continue;
-                const int per = __popc(r8), cnt = (int)__popcll(m) * per;
-                if (n + cnt > kCap) {
-                    wave_lds_sync();
-                    chain_pair_passes<MULTI, true>(P, n, c0, sRec, W, lane, pos, dir);
-                    wave_lds_sync();
-                    n = 0;
-                }
-                if ((cm >> j) & 1u) {
-                    int e = n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) * per;
-                    for (unsigned r = r8; r; r &= r - 1)
-                        W.pair[e++] = (unsigned short)(lane | ((k * kClusterSize + __builtin_ctz(r)) << 6));
-                }
-                n += cnt;
-            }
         } else {
             for (int k = 0; k < nCl; ++k) {
                 const unsigned long long m = __ballot((cm >> k) & 1u);
@@ -1979,7 +1942,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                     continue;
                 if (n + (int)__popcll(m) > kCap) {
                     wave_lds_sync();
-                    chain_pair_passes<MULTI, false>(P, n, c0, sRec, W, lane, pos, dir);
+                    chain_pair_passes<MULTI>(P, n, c0, sRec, W, lane, pos, dir);
                     wave_lds_sync();
                     n = 0;
                 }
@@ -1993,12 +1956,10 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         wave_lds_sync();
         DSECT_END(dc4, 4);
         DSECT_BEGIN(dc5);
-        if (table && RTC_TABLE_CL)
+        if (table)
             chain_pair_passes_cl(n, sRec, W, lane, pos, dir);
-        else if (table)
-            chain_pair_passes<MULTI, true>(P, n, c0, sRec, W, lane, pos, dir);
         else
-            chain_pair_passes<MULTI, false>(P, n, c0, sRec, W, lane, pos, dir);
+            chain_pair_passes<MULTI>(P, n, c0, sRec, W, lane, pos, dir);
         wave_lds_sync(); /* the pair list is rewritten by the next chunk */
         DSECT_END(dc5, 5);
     }
@@ -2112,20 +2073,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
-#if RTC_BM_LDS
-    /* the certified Box-Muller tables (rtc_bm_tables.h), read at lane-varying indices at every hit */
-    __shared__ rtcmath::BmLogEntry sBmLog[128];
-    __shared__ double sBmCos[64][2];
-    for (int i = threadIdx.x; i < 128; i += kChainBlock)
-        sBmLog[i] = rtcmath::kBmLogTab[i];
-    for (int i = threadIdx.x; i < 64; i += kChainBlock) {
-        sBmCos[i][0] = rtcmath::kBmCosTab[i][0];
-        sBmCos[i][1] = rtcmath::kBmCosTab[i][1];
-    }
-#define RTC_BM_TABS , sBmLog, sBmCos
-#else
-#define RTC_BM_TABS
-#endif
     if (threadIdx.x == 0)
         sWork = 0;
     sPow.fill(threadIdx.x);
@@ -2262,7 +2209,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             M = P.mats[c.idx];
                         }
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
-                        const V3 diffuseDir = normalized(add(normal, random_direction(rng RTC_BM_TABS)));
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
                         const V3 specularDir = reflect(dir, normal);
                         dir = lerp(diffuseDir, specularDir, M.smoothness);
                         pos = hitPoint;
