@@ -12,5 +12,8 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-AB_REPS=3 step ab 900 bash tools/ab_bench_libs.sh librtc.so librtc_su1.so librtc_su4.so || exit $?
+step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
+AB_REPS=3 step ab 900 bash tools/ab_bench_libs.sh librtc.so librtc_grp0.so librtc_grp_accb0.so || exit $?
+cd /tmp
+step loop1 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
 echo done
