@@ -621,6 +621,7 @@ template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 constexpr int kGeoLists = 16, kGeoCountStride = 32; /* ints: one 128-B line per counter */
 
+
 /* The pixel a lane renders and its primary ray (rowThread, main.c:88-94).  A 256-thread workgroup covers
  * 16x16 pixels of the launch's rows; wave w of it the 8x8 tile (w & 1, w >> 1). */
 struct PixelRay {
@@ -1763,12 +1764,26 @@ constexpr size_t kChainLdsBudget = 160 * 1024 / RTC_CHAIN_WGS_PER_CU;
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records; the owner's ray
  * by ds_bpermute from the owner lane (every lane takes part), the exact-safe filter, the reference arithmetic for
  * survivors, an atomic lexicographic minimum into the owner's key. */
+/* The clustered records staged in LDS structure-of-arrays: 16-B quarter k of record i at q[k * n + i], n = the
+ * staged record count.  Lanes reading different records then hit different banks in ds_read_b128's 16-lane
+ * groups (64-B records at lane-varying indices put four lanes of a group on each bank); one record is still four
+ * ds_read_b128. */
+__device__ __forceinline__ DevTri rec_soa(const float4 *__restrict__ q, int n, int i)
+{
+    DevTri t;
+    float4 *v = (float4 *)&t;
+    v[0] = q[i];
+    v[1] = q[n + i];
+    v[2] = q[2 * n + i];
+    v[3] = q[3 * n + i];
+    return t;
+}
 __device__ __forceinline__ float bperm_f(int srcLane, float v)
 {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane << 2, __float_as_int(v)));
 }
 template <bool MULTI>
-__device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, int c0, const DevTri *__restrict__ sRec,
+__device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, int c0, const float4 *__restrict__ sRec,
                                                   ChainWaveLds &W, int lane, V3 pos, V3 dir)
 {
     for (int b = 0; b < n; b += 64) {
@@ -1779,15 +1794,17 @@ __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, 
         const V3 rdir{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
         if (i < n) {
             Closest c{999999.f, -1};
-            const DevTri *R = (MULTI ? P.clTris : sRec) + (c0 + (int)(pr >> 6)) * kClusterSize;
+            const int r0 = (c0 + (int)(pr >> 6)) * kClusterSize, nRec = P.clusterCount * kClusterSize;
+            auto rec = [&](int j) -> DevTri { return MULTI ? P.clTris[r0 + j] : rec_soa(sRec, nRec, r0 + j); };
             unsigned surv = 0;
 #pragma unroll RTC_CHAIN_UNROLL
             for (int j = 0; j < kClusterSize; ++j)
-                surv |= (unsigned)general_filter(rpos, rdir, R[j]) << j;
+                surv |= (unsigned)general_filter(rpos, rdir, rec(j)) << j;
             while (surv) {
                 const int j = __builtin_ctz(surv);
                 surv &= surv - 1;
-                general_exact(rpos, rdir, R[j], __float_as_int(R[j].pad0), c);
+                const DevTri R = rec(j);
+                general_exact(rpos, rdir, R, __float_as_int(R.pad0), c);
             }
             if (c.idx >= 0 && c.dst < 999999.f)
                 atomicMin(&W.key[o], ((unsigned long long)__float_as_uint(c.dst) << 32) | (unsigned)c.idx);
@@ -1797,8 +1814,8 @@ __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, 
 /* The first-bounce pairs as (lane, live cluster j) -- one entry per cluster a lane keeps, the pass
  * looping over that cluster's records reachable from p0 (W.cl[j][1]: z = cluster index, w = reach bits); one
  * atomic per entry instead of one per record */
-__device__ __forceinline__ void chain_pair_passes_cl(int n, const DevTri *__restrict__ sRec, ChainWaveLds &W, int lane,
-                                                     V3 pos, V3 dir)
+__device__ __forceinline__ void chain_pair_passes_cl(int n, const float4 *__restrict__ sRec, int nRec, ChainWaveLds &W,
+                                                     int lane, V3 pos, V3 dir)
 {
     for (int b = 0; b < n; b += 64) {
         const int i = b + lane;
@@ -1808,10 +1825,10 @@ __device__ __forceinline__ void chain_pair_passes_cl(int n, const DevTri *__rest
         const V3 rdir{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
         if (i < n) {
             const float4 kb = W.cl[pr >> 6][1];
-            const DevTri *R = sRec + __float_as_int(kb.z) * kClusterSize;
+            const int r0 = __float_as_int(kb.z) * kClusterSize;
             Closest c{999999.f, -1};
             for (unsigned r = (unsigned)__float_as_int(kb.w); r; r &= r - 1) {
-                const DevTri &T = R[__builtin_ctz(r)];
+                const DevTri T = rec_soa(sRec, nRec, r0 + __builtin_ctz(r));
                 if (general_filter(rpos, rdir, T))
                     general_exact(rpos, rdir, T, __float_as_int(T.pad0), c);
             }
@@ -1823,7 +1840,7 @@ __device__ __forceinline__ void chain_pair_passes_cl(int n, const DevTri *__rest
 
 template <bool MULTI>
 __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, bool firstBounce, V3 pos,
-                                                     V3 dir, const DevTri *__restrict__ sRec, ChainWaveLds &W,
+                                                     V3 dir, const float4 *__restrict__ sRec, ChainWaveLds &W,
                                                      int lane, unsigned &tests)
 {
     W.key[lane] = kNoHitKey;
@@ -1851,7 +1868,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
             const int i = q * 64 + lane;
             bool can = false;
             if (i < P.clusterCount * kClusterSize) {
-                const DevTri &R = sRec[i];
+                const DevTri R = rec_soa(sRec, P.clusterCount * kClusterSize, i);
                 if (__float_as_int(R.pad0) >= 0) {
                     const V3 sv = sub(p0, V3{R.ax, R.ay, R.az});               /* raytracing.c:198 */
                     const V3 qv = cross(sv, V3{R.abx, R.aby, R.abz});          /* :202 */
@@ -1925,7 +1942,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                     continue;
                 if (n + (int)__popcll(m) > kCap) {
                     wave_lds_sync();
-                    chain_pair_passes_cl(n, sRec, W, lane, pos, dir);
+                    chain_pair_passes_cl(n, sRec, P.clusterCount * kClusterSize, W, lane, pos, dir);
                     wave_lds_sync();
                     n = 0;
                 }
@@ -1957,7 +1974,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc4, 4);
         DSECT_BEGIN(dc5);
         if (table)
-            chain_pair_passes_cl(n, sRec, W, lane, pos, dir);
+            chain_pair_passes_cl(n, sRec, P.clusterCount * kClusterSize, W, lane, pos, dir);
         else
             chain_pair_passes<MULTI>(P, n, c0, sRec, W, lane, pos, dir);
         wave_lds_sync(); /* the pair list is rewritten by the next chunk */
@@ -2046,7 +2063,7 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
  * (P.chainPrimF), the primary filter records.  (Staging the primary exact records and the shading records as well
  * measured no faster.) */
 struct ChainStage {
-    DevTri *rec;
+    float4 *rec; /* structure-of-arrays (rec_soa) */
     DevPrimF *primF;
 };
 template <bool MULTI>
@@ -2054,11 +2071,15 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
 {
     ChainStage S{nullptr, nullptr};
     if (!MULTI)
-        S.rec = (DevTri *)sDyn;
+        S.rec = (float4 *)sDyn;
     if (P.chainPrimF)
         S.primF = (DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
-    for (int i = threadIdx.x; S.rec && i < P.clusterCount * kClusterSize; i += kChainBlock)
-        S.rec[i] = P.clTris[i];
+    const int nRec = P.clusterCount * kClusterSize;
+    for (int i = threadIdx.x; S.rec && i < nRec; i += kChainBlock) {
+        const float4 *g = (const float4 *)(P.clTris + i);
+        for (int k = 0; k < 4; ++k)
+            S.rec[k * nRec + i] = g[k];
+    }
     for (int i = threadIdx.x; S.primF && i < P.triPadded; i += kChainBlock)
         S.primF[i] = P.primF[i];
     return S;
@@ -2077,7 +2098,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         sWork = 0;
     sPow.fill(threadIdx.x);
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
-    const DevTri *sRec = S.rec;
+    const float4 *sRec = S.rec;
     /* the staged primary filter records: always the LDS address (never null), used when P.chainPrimF */
     const DevPrimF *sPF = (const DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
     const bool pfStaged = P.chainPrimF != 0;
@@ -2092,13 +2113,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     ChainWaveLds &W = sWave[threadIdx.x >> 6];
     const RngJump laneJump = rng_jump_by(7u * (unsigned)lane); /* s -> the state 7 lane draws later */
     /* the geometry pixels: kGeoLists sub-lists from rtc_tile_cull, taken as one concatenated index space
-     * (l: the sub-list of item `it`, base: its first item, cnt: its length).  Workgroup b owns the items
-     * b + k * gridDim.x; its waves take the next k from an LDS counter, so a wave that drew cheap pixels takes
-     * more of them (a global counter would serialise ~80 k same-address atomics across the XCDs).  A wave's
-     * items increase, as the sub-list walk needs. */
+     * (l: the sub-list of item `it`, base: its first item).  Workgroup b owns the items b + k * gridDim.x; its
+     * waves take the next k from an LDS counter, so a wave that drew cheap pixels takes more of them (a global
+     * counter would serialise ~80 k same-address atomics across the XCDs; per-XCD returning counters, round 3,
+     * shortened the kernel 4 % but made every workgroup retire at its end, so the sky pass no longer filled the
+     * tail: frame 0.396 -> 0.42 ms). */
     int nextIt = 0;
+#define RTC_NEXT_ITEM() ((int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x)
     if (lane == 0)
-        nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
+        nextIt = RTC_NEXT_ITEM();
     const int tilesX = P.blocksX * 2;
     constexpr bool counting = COUNT;
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
@@ -2106,19 +2129,25 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #ifdef RTC_DIAG
     unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
 #endif
-    int l = 0, base = 0, cnt = __builtin_amdgcn_readfirstlane(KCONST(P.geoCount)[0]);
+    /* the sub-lists' inclusive prefix counts, lane l < kGeoLists holding sub-list l's, loaded once per wave: an
+     * item's sub-list is then a ballot, not a chain of dependent count loads as a wave's items pass the sub-lists */
+    int incl = lane < kGeoLists ? P.geoCount[lane * kGeoCountStride] : 0;
+#pragma unroll
+    for (int d = 1; d < kGeoLists; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d)
+            incl += v;
+    }
+    const int nItems = __builtin_amdgcn_readlane(incl, kGeoLists - 1);
     for (;;) {
         DSECT_BEGIN(dset);
         const int it = __builtin_amdgcn_readfirstlane(nextIt);
-        while (it - base >= cnt && l < kGeoLists - 1) {
-            base += cnt;
-            ++l;
-            cnt = __builtin_amdgcn_readfirstlane(KCONST(P.geoCount)[l * kGeoCountStride]);
-        }
-        if (it - base >= cnt)
+        if (it >= nItems)
             break;
+        const int l = (int)__popcll(__ballot(lane < kGeoLists && incl <= it));
+        const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
         if (lane == 0)
-            nextIt = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
+            nextIt = RTC_NEXT_ITEM();
         const int code = __builtin_amdgcn_readfirstlane(KCONST(P.geoList)[(size_t)l * P.geoCap + (it - base)]);
         const int tile = code >> 6, bit = code & 63;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One rank's share of a frame at N GPUs (rows y = r + kN), rendered on one GPU: the per-rank device time that
 bounds strong scaling (the gather of the uint8 parts and the re-interleave come on top).  Not part of the product.
-Usage: scale_probe.py [frames] [W H spp] [kernel: chain|overlap]  (overlap: the chain kernel with frame
+Usage: scale_probe.py [frames] [W H spp] [kernel: chain|overlap|overlap_inline]  (SCALE_NS=1,8: the N to probe; overlap: the chain kernel with frame
 pipelining, RTC_F_OVERLAP -- the per-frame period of back-to-back frames instead of one frame's latency)"""
 import json
 import os
@@ -18,7 +18,8 @@ from conftest import load_tris  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 kernel = sys.argv[5] if len(sys.argv) > 5 else "chain"
-extra = {"chain": {}, "overlap": {"overlap": True}}[kernel]
+extra = {"chain": {}, "overlap": {"overlap": True}, "overlap_inline": {"overlap": True, "chain_inline": True}}[kernel]
+NS = tuple(int(v) for v in os.environ.get("SCALE_NS", "1,2,4,8").split(","))
 tris, _ = load_tris("ultracomplex")
 scene, cam = rt.default_scene(), rt.camera_basis()
 ds = rt.DeviceScene(tris, None)
@@ -29,13 +30,13 @@ for _ in range(20):  # clocks settle
                          stream.cuda_stream)
 torch.cuda.synchronize()
 base = None
-for n in (1, 2, 4, 8):
+for n in NS:
     worst = 0.0
     per = []
     for r in range(n):  # every rank's share: the slowest sets the frame
         cfg = rt.RenderConfig(W, H, SPP, 10, True, row_start=r, row_stride=n, **extra)
         times = []
-        if kernel == "overlap":  # the period of 20 back-to-back pipelined frames (device synchronised around them)
+        if kernel.startswith("overlap"):  # the period of 20 back-to-back pipelined frames (device synchronised around them)
             for _ in range(frames):
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
