@@ -75,7 +75,8 @@ typedef struct RtcRenderDesc {
 #define RTC_F_PIPE          0x200 /* removed: RTC_EINVAL */
 #define RTC_F_SPEC          0x100 /* removed: RTC_EINVAL */
 #define RTC_F_CHAIN_INLINE  0x400 /* rtc_render_chain adds each pixel's samples itself instead of deferring the
-                                     in-order sum to a separate pass (A/B timing; identical frame) */
+                                     in-order sum to a separate pass (identical frame; the default for a small share
+                                     of a row-partitioned frame: rowStride > 1 and width * rows <= 400,000) */
 #define RTC_F_HOST_ROWS     0x1000 /* rtc_render_multi only: no gather -- every device copies its rows straight into
                                       their places of the host frame (rtc_copy_rows_d2h_dma, its own PCIe link);
                                       without it the parts are gathered to device 0 over RCCL, re-interleaved there

@@ -1715,6 +1715,7 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
  * Work: one wave per geometry pixel, from the tile cull's sub-lists (see the kernel). */
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
+constexpr size_t kInlineSumPixels = 400000;          /* shares (row stride > 1) up to this many pixels sum in-kernel */
 constexpr int kChainBlock = 256;
 #ifndef RTC_CHAIN_WORKERS
 #define RTC_CHAIN_WORKERS 1024 /* = the resident capacity (4 workgroups per CU): no second round of workgroups */
@@ -2169,8 +2170,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             }
         }
         DSECT_END(dset, 15);
-        f2 accxy{0.f, 0.f}; /* the pixel's accumulator (main.c:97): x, y packed, z */
-        float accz = 0.f;
+        /* in-kernel sums (items without a deferred slot): the pixel's accumulator (main.c:97), component c in lane c */
+        float acc = 0.f;
         int k = 0;       /* samples accumulated */
         unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
         while (k < P.spp && P.maxBounce > 0) {
@@ -2271,6 +2272,21 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
             int p = 0;
             SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+            /* in-kernel sums: the window's samples are staged in sample order in LDS -- the pair list's space, free
+             * until the next window's bounces; component c at stage[64 c + i] -- and lane c then adds them in order */
+            float *const stage = (float *)W.pair;
+            int staged = 0;
+            auto flush = [&]() {
+                wave_lds_sync();
+                if (lane < 3) {
+                    const float *src = stage + 64 * lane;
+#pragma unroll 8
+                    for (int i = 0; i < staged; ++i)
+                        acc = acc + src[i];
+                }
+                wave_lds_sync();
+                staged = 0;
+            };
             while (k < P.spp && p < nAct) {
                 const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
                 const unsigned long long notOne = ~ones & win;
@@ -2281,11 +2297,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     if (lane >= p && lane < p + take)
                         slot[k + lane - p] = SampleSlot{t.x, t.y, t.z};
                 } else {
-                    for (int b = p; b < p + take; ++b) {
-                        accxy = accxy + f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), b)),
-                                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), b))};
-                        accz = accz + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), b));
+                    if (lane >= p && lane < p + take) {
+                        const int i = staged + lane - p;
+                        stage[i] = t.x;
+                        stage[64 + i] = t.y;
+                        stage[128 + i] = t.z;
                     }
+                    staged += take;
                 }
                 mult += (lane >= p && lane < p + take) ? 1u : 0u;
                 k += take;
@@ -2301,11 +2319,18 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 if (deferred) {
                     for (int kk = k + lane; kk < k + m; kk += 64)
                         slot[kk] = SampleSlot{qx, qy, qz};
-                } else {
-                    for (int b = 0; b < m; ++b) {
-                        accxy = accxy + f2{qx, qy};
-                        accz = accz + qz;
+                } else if (m == 1) {
+                    if (lane == q) {
+                        stage[staged] = t.x;
+                        stage[64 + staged] = t.y;
+                        stage[128 + staged] = t.z;
                     }
+                    ++staged;
+                } else { /* the staged samples first, then this one m times */
+                    flush();
+                    const float v = lane == 0 ? qx : (lane == 1 ? qy : qz);
+                    for (int b = 0; b < m; ++b)
+                        acc = acc + v;
                 }
                 mult += lane == q ? (unsigned)m : 0u;
                 k += m;
@@ -2313,6 +2338,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     break;
                 p = q + hq;
             }
+            if (!deferred)
+                flush();
             jn += (unsigned)p;
 #ifdef RTC_DIAG
             dWindows++;
@@ -2333,16 +2360,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         if (deferred) {
             if (lane == 0)
                 P.itemPix[it] = r * P.width + x;
-        } else if (lane == 0) {
-            const size_t o = (size_t)r * (size_t)P.width + (size_t)x;
-            P.colors[3 * o] = float_to_u8(accxy.x);
-            P.colors[3 * o + 1] = float_to_u8(accxy.y);
-            P.colors[3 * o + 2] = float_to_u8(accz);
-            if (P.accum) {
-                P.accum[3 * o] = accxy.x;
-                P.accum[3 * o + 1] = accxy.y;
-                P.accum[3 * o + 2] = accz;
-            }
+        } else if (lane < 3) {
+            const size_t o = 3 * ((size_t)r * (size_t)P.width + (size_t)x) + (size_t)lane;
+            P.colors[o] = float_to_u8(acc);
+            if (P.accum)
+                P.accum[o] = acc;
         }
     }
 #ifdef RTC_DIAG
@@ -2515,8 +2537,12 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.geoList = P.geoCount + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
-         * (pixels beyond it are accumulated inside rtc_render_chain; same result) */
-        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE)) {
+         * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
+         * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
+         * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
+         * 4K 1/8 share are faster deferred) */
+        const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
+        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare) {
             const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;

@@ -286,6 +286,34 @@ def test_row_partition_and_deinterleave(gpu_available):
     ds.close()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+def test_small_shares_sum_in_kernel(overlap, gpu_available):
+    """The bench's 8-GPU shares of the 1080p x64 headline frame (rows y = r + 8k, 135 rows: small enough that
+    rtc_render_chain sums each pixel's samples itself instead of the deferred pass) equal the single-GPU frame,
+    which sums deferred, bit for bit in floats and bytes; with and without frame pipelining."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, G = 1920, 1080, 8
+    ref, racc, _ = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, 64, 10, True), want_accum=True)
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.current_stream().cuda_stream
+    rows = (H + G - 1) // G
+    out = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
+    acc = torch.zeros((G, rows, W, 3), dtype=torch.float32, device="cuda")
+    for r in range(G):
+        cfg = rt.RenderConfig(W, H, 64, 10, True, row_start=r, row_stride=G, overlap=overlap)
+        ds.render_rows_async(scene, cam, cfg, out[r].data_ptr(), acc[r].data_ptr(), None, st)
+    torch.cuda.synchronize()
+    ds.close()
+    o, a = out.cpu().numpy(), acc.cpu().numpy()
+    for r in range(G):
+        n = len(range(r, H, G))
+        assert np.array_equal(o[r, :n], ref[r::G]), f"rank {r} bytes"
+        assert np.array_equal(_bits(a[r, :n]), _bits(racc[r::G])), f"rank {r} floats"
+
+
 def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     """One device-resident scene across launches of growing and shrinking frames (per-launch scratch regrown,
     counter slots re-zeroed by the reduce kernel): every frame and segment count equals a fresh rtc_render;
