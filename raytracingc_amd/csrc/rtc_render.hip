@@ -145,6 +145,13 @@ struct __attribute__((aligned(32))) DevCluster {
     float alpha, beta, gammaE, e; /* the eps terms above: alpha, beta, gamma*E (or +inf: never cull), E */
 };
 
+/* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
+constexpr int kSkySlots = 8;
+struct SkyKey {
+    const void *colors, *accum;
+    float cam[13], env[14];
+    int dims[8];
+};
 struct RtcDeviceScene {
     int device;
     int triCount, triPadded, sphereCount; /* triPadded: multiple of kUnroll, zero (never-hit) records */
@@ -162,11 +169,13 @@ struct RtcDeviceScene {
      * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
     unsigned char *scratch;
     size_t scratchCap; /* bytes */
-    /* RTC_F_OVERLAP: launches alternate between two halves of the scratch; skyPending[h]: a sky pass that reads
-     * half h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends) */
-    int flip;
-    bool skyPending[2];
-    hipEvent_t evSkyDone[2], evGeoDone;
+    /* RTC_F_OVERLAP: launches cycle through kSkySlots slots of the scratch; skyPending[h]: a sky pass that reads
+     * slot h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends; skyKey[h]: the rows,
+     * camera and environment it writes); lastSky: the slot of the newest one */
+    int flip, lastSky;
+    bool skyPending[kSkySlots];
+    SkyKey skyKey[kSkySlots];
+    hipEvent_t evSkyDone[kSkySlots], evGeoDone;
     hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
     /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
      * sample order at the kernel's end by the wave that rendered the pixel (grown on demand, <= kSampleBufBudget
@@ -475,9 +484,11 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
-    for (hipEvent_t *ev : {&s->evSkyDone[0], &s->evSkyDone[1], &s->evGeoDone})
+    for (int h = 0; h < kSkySlots; ++h)
         if (e == hipSuccess)
-            e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+            e = hipEventCreateWithFlags(&s->evSkyDone[h], hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&s->evGeoDone, hipEventDisableTiming);
     for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
         if (e == hipSuccess)
             e = hipEventCreate(ev);
@@ -524,7 +535,10 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
         (void)hipEventDestroy(s->evJoin);
-    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evSkyDone[0], s->evSkyDone[1], s->evGeoDone})
+    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evGeoDone})
+        if (ev)
+            (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : s->evSkyDone)
         if (ev)
             (void)hipEventDestroy(ev);
     if (s->side)
@@ -2385,6 +2399,25 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
 }
 
+static SkyKey sky_key(const RenderParams &P)
+{
+    SkyKey k;
+    memset(&k, 0, sizeof k);
+    k.colors = P.colors;
+    k.accum = P.accum;
+    const V3 c[4] = {P.origin, P.ex, P.ey, P.ez}, e[4] = {P.env.sun, P.env.horizon, P.env.zenith, P.env.ground};
+    for (int i = 0; i < 4; ++i) {
+        k.cam[3 * i] = c[i].x, k.cam[3 * i + 1] = c[i].y, k.cam[3 * i + 2] = c[i].z;
+        k.env[3 * i] = e[i].x, k.env[3 * i + 1] = e[i].y, k.env[3 * i + 2] = e[i].z;
+    }
+    k.cam[12] = P.fov;
+    k.env[12] = P.env.focus;
+    k.env[13] = P.env.intensity;
+    const int dims[8] = {P.width, P.height, P.rows, P.rowStart, P.rowStride, P.spp, P.maxBounce, P.hoist};
+    memcpy(k.dims, dims, sizeof dims);
+    return k;
+}
+
 static EnvParams env_of(const Scene &s)
 {
     EnvParams e{};
@@ -2482,34 +2515,45 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * that counts segments joins, the reduction reads the sky kernel's counters) */
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
     RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
-    const int half = overlap ? s->flip : 0; /* the scratch half this launch writes */
+    const int half = overlap ? s->flip : 0; /* the scratch slot this launch writes */
     /* The hooks are one-shot: this launch records the events armed before it and forgets them, so a later launch
      * never records an event its caller has since released (rtc_scene_set_geometry_event / _frame_event). */
     const hipEvent_t geoEvent = s->geoEvent, frameEvent = s->frameEvent;
     ms->geoEvent = nullptr;
     ms->frameEvent = nullptr;
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
-     * scratch half.  A launch that is not itself overlapped waits for every such pass before its first kernel:
+     * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
-     * overlapped launch waits for the pass on the half it rewrites here, and for the other half before its
-     * geometry kernel (below). */
-    for (int h = 0; h < 2; ++h)
-        if (s->skyPending[h] && (!overlap || h == half)) {
-            HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[h], 0));
+     * overlapped launch waits when a pending pass reads the slot it rewrites, or writes the same Color or
+     * accumulator buffer with other rows, camera or environment (the same ones write the same sky pixels with the
+     * same values, and never a pixel this launch's geometry kernel writes).  One wait, on the newest pass, covers
+     * every earlier one (the side stream runs them in order), so with kSkySlots slots a pipelined sequence of one
+     * camera waits once every kSkySlots - 1 launches: each wait is a cross-stream hop of ~10 us before the next
+     * kernel (round 3: waiting before every geometry kernel cost 0.107 vs 0.098 ms per 1080p 1/8 share). */
+    const SkyKey key = sky_key(P);
+    bool mustWait = false;
+    for (int h = 0; h < kSkySlots; ++h)
+        if (s->skyPending[h])
+            mustWait = mustWait || !overlap || h == half ||
+                       ((s->skyKey[h].colors == key.colors || (key.accum && s->skyKey[h].accum == key.accum)) &&
+                        memcmp(&s->skyKey[h], &key, sizeof key) != 0);
+    if (mustWait) {
+        HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[s->lastSky], 0));
+        for (int h = 0; h < kSkySlots; ++h)
             ms->skyPending[h] = false;
-        }
+    }
     size_t halfBytes = 0;
     if (cull) {
         const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + blocks + 4) * sizeof(int) +
                             (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int); /* + sub-lists */
         halfBytes = (need + 255) & ~(size_t)255;
-        if (2 * halfBytes > s->scratchCap) { /* both halves (hipFree synchronises the device: no pass still reads them) */
+        if (kSkySlots * halfBytes > s->scratchCap) { /* every slot (hipFree synchronises the device: no pass reads them) */
             if (ms->scratch)
                 HIP_TRY(hipFree(ms->scratch));
             ms->scratch = nullptr;
             ms->scratchCap = 0;
-            HIP_TRY(hipMalloc(&ms->scratch, 2 * halfBytes));
-            ms->scratchCap = 2 * halfBytes;
+            HIP_TRY(hipMalloc(&ms->scratch, kSkySlots * halfBytes));
+            ms->scratchCap = kSkySlots * halfBytes;
         }
     }
     P.blocksX = (int)grid.x;
@@ -2571,15 +2615,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             /* the split launch: the sky pixels on the side stream, concurrently with rtc_render_chain over the
              * geometry pixels (the tile cull's sub-lists) on `st`; `st` then waits for both */
             hipStream_t skyStream = RTC_SIDE_STREAM ? s->side : st;
-            /* RTC_F_OVERLAP: the previous launch's sky pass (reading the other scratch half) ends before this
-             * launch's passes start -- its prep and tile cull above overlapped it -- so that the persistent
-             * geometry workgroups all find the chip free and are dispatched first, as in a joined launch (the
-             * fork below follows this wait: a sky pass queued right behind the previous one would otherwise
-             * take the chip first) */
-            if (overlap && s->skyPending[half ^ 1]) {
-                HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[half ^ 1], 0));
-                ms->skyPending[half ^ 1] = false;
-            }
+            /* (RTC_F_OVERLAP: the geometry kernel does not wait for the previous launch's sky pass -- in the
+             * pipelined steady state it has ended by the time this tile cull does, and the wait was a ~10 us
+             * cross-stream hop on every frame; round 2 waited here so that the persistent geometry workgroups
+             * found the chip free) */
             if (RTC_SIDE_STREAM) {
                 HIP_TRY(hipEventRecord(s->evFork, st));
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
@@ -2592,9 +2631,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evSky1, skyStream));
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
-            if (overlap) { /* this sky pass reads scratch half `half` until evSkyDone[half] */
+            if (overlap) { /* this sky pass reads scratch slot `half` until evSkyDone[half] */
                 HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
                 ms->skyPending[half] = true;
+                ms->skyKey[half] = key;
+                ms->lastSky = half;
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
@@ -2633,7 +2674,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
                 if (frameEvent)
                     HIP_TRY(hipEventRecord(frameEvent, s->side));
-                ms->flip ^= 1;
+                ms->flip = (ms->flip + 1) % kSkySlots;
                 return 0;
             }
             if (RTC_SIDE_STREAM)

@@ -394,6 +394,38 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
     ds.close()
 
 
+def test_overlap_slot_ring(gpu_available):
+    """RTC_F_OVERLAP launches cycle through 8 scratch slots and wait for the unjoined sky passes only when one reads
+    the slot being rewritten or writes the same buffer with another camera: 20 back-to-back frames of one camera
+    into one buffer (two waits), then 21 alternating between two cameras into one buffer (a wait each), then a
+    share of the frame into the same buffer: each final buffer equals a joined render."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene = rt.default_scene()
+    cams = [rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1)]
+    W, H, spp = 320, 180, 8
+    ref = [rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))[0] for c in cams]
+    cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True)
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    for _ in range(20):
+        ds.render_rows_async(scene, cams[1], cfg, buf.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), ref[1])
+    for k in range(21):  # cams[1], cams[0], ..., the last one cams[1]
+        ds.render_rows_async(scene, cams[(k + 1) % 2], cfg, buf.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), ref[1])
+    share = rt.RenderConfig(W, H, spp, 10, True, overlap=True, row_start=1, row_stride=2)
+    part = buf[: (H + 1) // 2]
+    ds.render_rows_async(scene, cams[0], share, part.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(part.cpu().numpy()[: H // 2], ref[0][1::2])
+    ds.close()
+
+
 def test_overlap_with_counters_and_mixed_launches(gpu_available):
     """An RTC_F_OVERLAP launch that asks for segment counters joins (the counts equal a joined launch's), and
     joined / overlapped / no-tile-cull launches interleaved on one scene (the scratch halves and pending sky
