@@ -145,6 +145,12 @@ struct __attribute__((aligned(32))) DevCluster {
     float alpha, beta, gammaE, e; /* the eps terms above: alpha, beta, gamma*E (or +inf: never cull), E */
 };
 
+/* The scene's own events only order its two streams on one device (the caller's frame / geometry events keep their
+ * flags): no system-scope fence when they are recorded (RTC_ORDER_FENCE 1 restores it) */
+#ifndef RTC_ORDER_FENCE
+#define RTC_ORDER_FENCE 0
+#endif
+constexpr unsigned kOrderEventFlags = hipEventDisableTiming | (RTC_ORDER_FENCE ? 0u : hipEventDisableSystemFence);
 /* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
 constexpr int kSkySlots = 8;
 struct SkyKey {
@@ -481,14 +487,14 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     if (e == hipSuccess) /* the sky tiles yield to the heavy tiles */
         e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, leastPrio);
     if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evFork, hipEventDisableTiming);
+        e = hipEventCreateWithFlags(&s->evFork, kOrderEventFlags);
     if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evJoin, hipEventDisableTiming);
+        e = hipEventCreateWithFlags(&s->evJoin, kOrderEventFlags);
     for (int h = 0; h < kSkySlots; ++h)
         if (e == hipSuccess)
-            e = hipEventCreateWithFlags(&s->evSkyDone[h], hipEventDisableTiming);
+            e = hipEventCreateWithFlags(&s->evSkyDone[h], kOrderEventFlags);
     if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evGeoDone, hipEventDisableTiming);
+        e = hipEventCreateWithFlags(&s->evGeoDone, kOrderEventFlags);
     for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
         if (e == hipSuccess)
             e = hipEventCreate(ev);
