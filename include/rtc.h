@@ -82,10 +82,12 @@ typedef struct RtcRenderDesc {
                                       without it the parts are gathered to device 0 over RCCL, re-interleaved there
                                       and copied once.  Same frame bit for bit. */
 #define RTC_F_OVERLAP       0x800 /* frame pipelining (device-resident split only): the launch does not make
-                                     `stream` wait for its sky pass, so the next launch on the same scene prepares
-                                     its frame (primary records, tile cull; double-buffered scratch) while this
-                                     one's sky pass still runs; the next geometry-pixel kernel waits for it, and a
-                                     next launch that is not overlapped waits for it before its first kernel.  The
+                                     `stream` wait for its sky pass, so the next launches on the same scene render
+                                     (scratch in 8 slots) while this one's sky pass still runs.  A later overlapped
+                                     launch waits for it only when it would rewrite its scratch slot (8 launches
+                                     later) or writes the same Color / accumulator buffer with other rows, camera or
+                                     environment; a later launch that is not overlapped waits for it before its
+                                     first kernel.  The
                                      frame is complete when the scene's frame event (rtc_scene_set_frame_event)
                                      fires; with segment counters requested the launch joins as usual.  Same
                                      frame bit for bit. */
