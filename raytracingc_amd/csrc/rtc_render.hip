@@ -16,6 +16,7 @@
  *  - quantisation (vec3ToColor) is fused; the float accumulator is written only when asked for.
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -2405,6 +2406,26 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
 }
 
+/* A kernel launch whose completion also records `stop` (null: a plain launch): the event is the dispatch's own
+ * completion signal, so the stream gets no separate marker packet -- each marker on the launch stream cost ~5-7 us
+ * before the next kernel (RTC_EXT_EVENTS 0: hipEventRecord after the launch) */
+#ifndef RTC_EXT_EVENTS
+#define RTC_EXT_EVENTS 1
+#endif
+template <typename... K, typename... A>
+static hipError_t launch_stop(void (*k)(K...), dim3 g, dim3 b, size_t sh, hipStream_t st, hipEvent_t stop, A... args)
+{
+    if (stop && RTC_EXT_EVENTS) {
+        hipExtLaunchKernelGGL(k, g, b, (std::uint32_t)sh, st, nullptr, stop, 0u, args...);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k, g, b, sh, st, args...);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && stop)
+        e = hipEventRecord(stop, st);
+    return e;
+}
+
 static SkyKey sky_key(const RenderParams &P)
 {
     SkyKey k;
@@ -2613,8 +2634,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
                            s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, P.geoCount);
     if (cull) {
-        hipLaunchKernelGGL(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st, P,
-                           mask, weight, tileW, pixMask);
+        /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
+        HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st,
+                            fused && RTC_SIDE_STREAM ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {
@@ -2626,7 +2648,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
              * cross-stream hop on every frame; round 2 waited here so that the persistent geometry workgroups
              * found the chip free) */
             if (RTC_SIDE_STREAM) {
-                HIP_TRY(hipEventRecord(s->evFork, st));
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
             }
             if (s->timing)
@@ -2651,22 +2672,23 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
             P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kChainLdsBudget;
             const size_t dyn = rec + (P.chainPrimF ? pf : 0);
-            if (s->chunkCount > 1) {
-                if (dSegments)
-                    hipLaunchKernelGGL((rtc_render_chain<true, true>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-                else
-                    hipLaunchKernelGGL((rtc_render_chain<true, false>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-            } else if (dSegments) {
-                hipLaunchKernelGGL((rtc_render_chain<false, true>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-            } else {
-                hipLaunchKernelGGL((rtc_render_chain<false, false>), dim3(kChainWorkers), dim3(kChainBlock), dyn, st, P);
-            }
-            HIP_TRY(hipGetLastError());
+            /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
+             * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
+            hipEvent_t chainStop = overlap && P.sampleCap == 0 ? s->evGeoDone : nullptr;
+            const dim3 cg(kChainWorkers), cb(kChainBlock);
+            if (s->chunkCount > 1 && dSegments)
+                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, st, chainStop, P));
+            else if (s->chunkCount > 1)
+                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, dyn, st, chainStop, P));
+            else if (dSegments)
+                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, dyn, st, chainStop, P));
+            else
+                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, st, chainStop, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
             if (P.sampleCap > 0) {
                 const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                hipLaunchKernelGGL(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, P);
+                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, overlap ? s->evGeoDone : nullptr, P));
                 HIP_TRY(hipGetLastError());
             }
             if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
@@ -2675,8 +2697,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             }
             ms->timed = s->timing;
             if (overlap) {
-                /* no join: the frame is complete once the side stream has passed both passes */
-                HIP_TRY(hipEventRecord(s->evGeoDone, st));
+                /* no join: the frame is complete once the side stream has passed both passes (evGeoDone: recorded
+                 * by the last kernel above) */
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
                 if (frameEvent)
                     HIP_TRY(hipEventRecord(frameEvent, s->side));
