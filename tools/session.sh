@@ -14,7 +14,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-tag=${1:-r03_h}
+tag=${1:-r03_i}
 bash tools/profile_workload.sh ultracomplex_1080p64 $tag || exit $?
 step digest_$tag 60 python tools/pmc_digest.py "$OUT/prof_ultracomplex_1080p64_$tag" ultracomplex_1080p64 || exit $?
 cp profiles/pmc_ultracomplex_1080p64.json "$OUT/pmc_ultracomplex_1080p64.json"
@@ -29,5 +29,11 @@ cd /tmp
 step loop1_$tag 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1_$tag" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
 step loop8_$tag 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop8_$tag" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 60 overlap 8 || exit $?
 cd "$R"
+# N > 1 rehearsal on this one GPU (gloo, ranks sharing the card: the host-frame path and the small-share launches, not
+# a scaling measurement -- the 8-GPU curve is the driver's)
+for n in 2 8; do
+  step rehearse${n}_$tag 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+    --master-port $((29500 + n)) bench.py --gpus $n --steps 20 --warmup 3 --no-cpu-baseline --no-extras || exit $?
+done
 step bench_$tag 400 python bench.py || exit $?
 echo done
