@@ -154,6 +154,7 @@ struct __attribute__((aligned(32))) DevCluster {
 constexpr unsigned kOrderEventFlags = hipEventDisableTiming | (RTC_ORDER_FENCE ? 0u : hipEventDisableSystemFence);
 /* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
 constexpr int kSkySlots = 8;
+constexpr int kGeoRing = 16, kGeoSetInts = 16 * 32; /* kGeoLists counters, 32 ints apart */
 struct SkyKey {
     const void *colors, *accum;
     float cam[13], env[14];
@@ -180,6 +181,17 @@ struct RtcDeviceScene {
      * slot h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends; skyKey[h]: the rows,
      * camera and environment it writes); lastSky: the slot of the newest one */
     int flip, lastSky;
+    /* rtc_render_chain's sub-list counters: a ring of kGeoRing sets, set q % kGeoRing for the q-th split launch;
+     * each launch's tile cull zeroes the next launch's set, so a launch on the same stream as the previous one
+     * needs no rtc_prep_primary to clear its counters (cullStream: that stream) */
+    int *geoCounts;
+    unsigned long long geoSeq;
+    hipStream_t cullStream;
+    bool cullValid;
+    /* rtc_prep_primary's records are for prepOrigin, written on prepStream (prepValid: they exist) */
+    bool prepValid;
+    float prepOrigin[3];
+    hipStream_t prepStream;
     bool skyPending[kSkySlots];
     SkyKey skyKey[kSkySlots];
     hipEvent_t evSkyDone[kSkySlots], evGeoDone;
@@ -477,6 +489,10 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     if (e == hipSuccess) /* kept zero between launches by rtc_reduce_segments */
         e = hipMemset(s->segSlots, 0, 256 * 16 * sizeof(unsigned long long));
     if (e == hipSuccess)
+        e = hipMalloc(&s->geoCounts, kGeoRing * kGeoSetInts * sizeof(int));
+    if (e == hipSuccess)
+        e = hipMemset(s->geoCounts, 0, kGeoRing * kGeoSetInts * sizeof(int));
+    if (e == hipSuccess)
         e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->mats, dm.data(), dm.size() * sizeof(DevMat), hipMemcpyHostToDevice);
@@ -538,6 +554,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->samples);
     if (s->segSlots)
         (void)hipFree(s->segSlots);
+    if (s->geoCounts)
+        (void)hipFree(s->geoCounts);
     if (s->evFork)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
@@ -586,8 +604,10 @@ struct RenderParams {
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
     /* rtc_render_chain's work: kGeoLists sub-lists of geometry pixels (tile*64 + bit), filled by rtc_tile_cull
      * (tile t appends to sub-list t % kGeoLists, one atomic per tile with geometry, spread over kGeoLists
-     * counters in separate cache lines); geoCount[l * 32] = entries of sub-list l, zeroed by rtc_prep_primary */
+     * counters in separate cache lines); geoCount[l * 32] = entries of sub-list l, zeroed by the previous split
+     * launch's rtc_tile_cull on the same stream, or by rtc_prep_primary */
     int *__restrict__ geoCount;
+    int *__restrict__ geoCountNext; /* the next split launch's counters, zeroed by this launch's rtc_tile_cull */
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
@@ -1183,6 +1203,8 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     }
     const int bx = blockIdx.x, by = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (P.geoCountNext && bx == 0 && by == 0 && threadIdx.x < kGeoLists) /* the next split launch's sub-lists */
+        P.geoCountNext[threadIdx.x * kGeoCountStride] = 0;
 #ifndef RTC_TILE_PREFILTER
 #define RTC_TILE_PREFILTER 1
 #endif
@@ -2604,8 +2626,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     unsigned *tileW = cull ? weight + blocks : nullptr;
     int *order = cull ? (int *)(tileW + tiles) : nullptr;
     if (chain) {
-        P.geoCount = order + blocks + 4;
-        P.geoList = P.geoCount + kGeoLists * kGeoCountStride;
+        P.geoCount = s->geoCounts + (size_t)(s->geoSeq % kGeoRing) * kGeoSetInts;
+        P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
+        P.geoList = order + blocks + 4 + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
@@ -2630,9 +2653,27 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             P.sampleCap = (int)cap;
         }
     }
-    if (s->triPadded > 0 || chain)
+    /* rtc_prep_primary: the primary records of this camera origin, and this launch's sub-list counters zeroed.  It
+     * is skipped when the records are already those of this origin (written on this stream) and the counters were
+     * zeroed by the previous split launch's tile cull on this stream -- frames of one camera position (round 3:
+     * a 5 us kernel at the head of every frame) */
+    const float org[3] = {P.origin.x, P.origin.y, P.origin.z};
+    const bool prepCurrent = s->prepValid && s->prepStream == st && memcmp(s->prepOrigin, org, sizeof org) == 0;
+    const bool countsZeroed = !chain || (s->cullValid && s->cullStream == st);
+    if ((s->triPadded > 0 || chain) && !(prepCurrent && countsZeroed)) {
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
-                           s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, P.geoCount);
+                           s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin,
+                           chain ? P.geoCount : nullptr);
+        HIP_TRY(hipGetLastError());
+        ms->prepValid = true;
+        ms->prepStream = st;
+        memcpy(ms->prepOrigin, org, sizeof org);
+    }
+    if (chain) {
+        ms->geoSeq++;
+        ms->cullValid = true;
+        ms->cullStream = st;
+    }
     if (cull) {
         /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
         HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st,
