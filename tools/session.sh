@@ -14,7 +14,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "   rc=$rc" | tee -a "$OUT/steps.log"
   return $rc
 }
-tag=${1:-r03_i}
+tag=${1:-r03_j}
 bash tools/profile_workload.sh ultracomplex_1080p64 $tag || exit $?
 step digest_$tag 60 python tools/pmc_digest.py "$OUT/prof_ultracomplex_1080p64_$tag" ultracomplex_1080p64 || exit $?
 cp profiles/pmc_ultracomplex_1080p64.json "$OUT/pmc_ultracomplex_1080p64.json"
