@@ -206,6 +206,13 @@ def kernel_roofline(name, live_ms, dg, work):
             e["valu_insts_per_launch"] = int(valu)
             e["fp64_insts_per_launch"] = int(f64)
             e["valu_issue_frac"] = round((2.0 * valu + 2.0 * f64) / (1024 * ms * 1e-3 * 2.4e9), 4)
+        gui = pd.get("GRBM_GUI_ACTIVE")
+        if valu and gui:
+            # the same issue slots over the kernel's own busy cycles in the PMC pass (rocprofv3 serialises dispatches
+            # while it collects counters, so the kernel runs alone): GRBM_GUI_ACTIVE / 8 XCDs cycles per SIMD
+            e["isolated_cycles"] = int(gui / 8)
+            e["isolated_ms_at_2p4ghz"] = round(gui / 8 / 2.4e9 * 1e3, 4)
+            e["valu_issue_frac_isolated"] = round((2.0 * valu + 2.0 * f64) / (1024 * gui / 8), 4)
         for c, key in (("SQ_INSTS_SALU", "salu_insts_per_launch"), ("SQ_INSTS_LDS", "lds_insts_per_launch"),
                        ("SQ_LDS_BANK_CONFLICT", "lds_bank_conflict_cycles_per_launch")):
             if c in pd:
@@ -233,9 +240,10 @@ def main():
     ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
                     help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
-    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
-                    help="N > 1: process group backend (auto: nccl = RCCL when every rank has its own GPU; gloo lets "
-                         "ranks share one GPU for a rehearsal, without the RCCL leg)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: process group backend.  nccl (= RCCL, the default) needs a GPU per rank; gloo is an "
+                         "explicit rehearsal mode in which ranks may share GPUs (no RCCL leg; the line then reports "
+                         "the distinct GPUs used and ranks_per_gpu)")
     args = ap.parse_args()
 
     import numpy as np
@@ -251,15 +259,19 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     ndev = torch.cuda.device_count()
+    multi = world > 1
+    if multi and args.backend == "nccl" and ndev < world:
+        raise SystemExit(f"{world} ranks but {ndev} GPU(s): the nccl (RCCL) backend needs one GPU per rank; pass "
+                         f"--backend gloo for a rehearsal with ranks sharing GPUs")
     gpu = local % ndev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    multi = world > 1
+    n_phys = min(world, ndev)  # distinct GPUs the ranks run on (one node)
     backend = None
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        backend = args.backend if args.backend != "auto" else ("nccl" if ndev >= world else "gloo")
+        backend = args.backend
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:
@@ -308,20 +320,20 @@ def main():
     cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
     cfg_r = rank_config(cfg_joined, rank, world)
 
-    def loop(cfg, frames):
-        return ds.frame_loop(scene, cam, cfg, [t.data_ptr() for t in dev_rows], host_ptr, pitch, frames,
+    def loop(cfg, frames, cams=None):
+        return ds.frame_loop(scene, cams or cam, cfg, [t.data_ptr() for t in dev_rows], host_ptr, pitch, frames,
                              stream.cuda_stream)
 
-    def timed(cfg, steps, warmup):
+    def timed(cfg, steps, warmup, cams=None):
         """warmup + steps pipelined frames (rtc_frame_loop: render with RTC_F_OVERLAP, each frame's rows copied into
         the host frame by the SDMA engines while the next frames render); the timed region spans the steps frames,
         barrier + device synchronisation on both sides, max over ranks."""
         if warmup:
-            loop(cfg, warmup)
+            loop(cfg, warmup, cams)
         barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        st = loop(cfg, steps)
+        st = loop(cfg, steps, cams)
         torch.cuda.synchronize(dev)
         barrier()
         dt = allreduce_max(time.perf_counter() - t0)
@@ -362,6 +374,19 @@ def main():
     # the last frame of the timed run as it landed in host memory (every rank's rows)
     frame_host = host_frame((args.steps - 1) % nbuf).copy() if rank == 0 else None
     barrier()
+
+    # a moving camera: the same pipelined frames (D2H included) over ORBIT_FRAMES distinct camera origins on an orbit
+    # around the default look-at point, so every frame re-derives its primary records and the frame-to-frame reuse of
+    # the static timed loop (the prep skip, the same-camera sky-pass wait elision) is never available
+    orbit = orbit_cameras(rt)
+    tm, _ = timed(cfg_r, args.steps, args.warmup, orbit)
+    frame_mov = host_frame((args.steps - 1) % nbuf).copy() if rank == 0 else None
+    barrier()
+    moving = {"ms_per_step": round(tm / args.steps * 1e3, 4), "value": round(samples * args.steps / tm / 1e6, 3),
+              "cameras": len(orbit),
+              "what": f"{args.steps} pipelined frames, frame k from camera k mod {len(orbit)} of an orbit of "
+                      f"+-{ORBIT_DEG:g} deg about the default look-at point (origins on a circle of the default "
+                      "camera's distance), render + SDMA D2H into the host frame, like the headline loop"}
 
     extras = {}
     if multi and backend == "nccl":
@@ -427,7 +452,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": n_phys,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t / args.steps * 1e3, 4),
@@ -440,7 +465,10 @@ def main():
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
                        "max_bounce": 10, "triangles": T,
                        "parallelism": f"rows mod {world}; each rank SDMA-copies its rows into the shared host frame"
-                                      + (f"; RCCL gather measured beside it ({backend})" if multi else ""),
+                                      + ("; RCCL gather to rank 0's GPU measured beside it (rccl_device_frame)"
+                                         if backend == "nccl" else "")
+                                      + (f"; REHEARSAL: {world} gloo ranks on {n_phys} GPU(s), no RCCL leg, not a "
+                                         "scaling measurement" if backend == "gloo" else ""),
                        "step": "render + D2H of Color[W*H] into pinned host memory (rtc_frame_loop: frames pipelined, "
                                "frame k+1's preparation overlapping frame k's sky pass; frame k's SDMA copy overlapping "
                                "the next frames' renders; triple-buffered)",
@@ -448,11 +476,14 @@ def main():
                                "environment)"},
             "roofline": {"bound": "valu", "dominant": dominant,
                          "achieved": dk.get("valu_issue_frac"), "peak": 1.0, "unit": "VALU issue fraction",
-                         "frac": frac, "traffic": dk.get("traffic"),
+                         "frac": frac, "frac_isolated": dk.get("valu_issue_frac_isolated"),
+                         "traffic": dk.get("traffic"),
                          "kernels": kernels,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
                          "note": "per kernel: ms = HIP events around it on its own stream (live); valu_issue_frac = "
-                                 "(2 x VALU + 2 x FP64 wave instructions) / (1024 SIMDs x 2.4 GHz x ms), counters from "
+                                 "(2 x VALU + 2 x FP64 wave instructions) / (1024 SIMDs x 2.4 GHz x ms), the span-based "
+                                 "fraction; valu_issue_frac_isolated = the same over GRBM_GUI_ACTIVE / 8 XCDs cycles of "
+                                 "the kernel's own dispatch in the PMC pass (it runs alone there); counters from "
                                  "the committed rocprofv3 PMC digest of this workload (roofline.kernels.*.source); "
                                  "frac_57flop = ray-triangle tests x 57 flop / ms / 157.3 TFLOP/s (SURVEY §8 d); "
                                  "traffic = counter HBM bytes per launch (traffic_note: which correction); "
@@ -472,6 +503,14 @@ def main():
         # the frame as it landed in host memory == one GPU rendering the whole frame through rtc_render
         ref1, gacc, _ = rt.render(tris, None, scene, cam, cfg_joined, device=gpu, want_accum=(world == 1))
         line["host_frame_equals_rtc_render"] = bool(np.array_equal(frame_host, ref1))
+        if multi:
+            line["ranks"] = world
+            line["ranks_per_gpu"] = round(world / n_phys, 3)
+            line["rehearsal"] = backend == "gloo"
+        mcam = orbit[(args.steps - 1) % len(orbit)]
+        refm, _, _ = rt.render(tris, None, scene, mcam, cfg_joined, device=gpu)
+        moving["last_frame_equals_rtc_render"] = bool(np.array_equal(frame_mov, refm))
+        line["moving_camera"] = moving
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(tris, tonly, scene, cam, W, H, spp, args.cpu_budget_samples, frame_host, gacc)
@@ -484,6 +523,24 @@ def main():
         shared.close(barrier)
     if multi:
         dist.destroy_process_group()
+
+
+ORBIT_FRAMES, ORBIT_DEG = 20, 15.0
+
+
+def orbit_cameras(rt):
+    """ORBIT_FRAMES cameras (main.c:252-255 bases) whose origins sweep +-ORBIT_DEG degrees about the default look-at
+    point in the horizontal plane, at the default camera's distance and height."""
+    ox, oy, oz = rt.DEFAULT_ORIGIN
+    lx, ly, lz = rt.DEFAULT_LOOKING_AT
+    r = math.hypot(ox - lx, oz - lz)
+    a0 = math.atan2(oz - lz, ox - lx)
+    cams = []
+    for k in range(ORBIT_FRAMES):
+        a = a0 + math.radians(-ORBIT_DEG + 2 * ORBIT_DEG * k / (ORBIT_FRAMES - 1))
+        cams.append(rt.camera_basis((lx + r * math.cos(a), oy, lz + r * math.sin(a)), rt.DEFAULT_LOOKING_AT,
+                                    rt.DEFAULT_FOV))
+    return cams
 
 
 def dataclasses_replace(cfg, **kw):

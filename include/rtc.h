@@ -112,6 +112,8 @@ typedef struct RtcStats {
 #define RTC_EIO (-10003)
 #define RTC_ENOMEM (-10004)
 #define RTC_EFORMAT (-10005)
+#define RTC_ETIMEDOUT (-10006) /* an SDMA copy did not complete in time and may still run (rtc_dma_pending) */
+#define RTC_EBUSY (-10007)     /* a range a timed-out copy may still write (rtc_host_unregister) */
 
 const char *rtc_last_error(void);
 const char *rtc_version(void);
@@ -205,6 +207,17 @@ int rtc_copy_async(void *dst, const void *src, size_t bytes, int blocks, void *s
  * frame's event first).  Unlike the runtime's D2H blit kernel it does not slow render kernels running at the
  * same time (~0.01 vs ~0.1 ms per 1080p frame). */
 int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes);
+/* Copy-engine timeouts (rtc_copy_d2h_dma, rtc_copy_rows_d2h_dma, rtc_frame_loop): a copy that has not completed after
+ * 20 s (RTC_DMA_TIMEOUT_MS overrides) returns RTC_ETIMEDOUT, but the engine may still read its source and write its
+ * destination.  The library keeps such a copy listed (its completion signal is neither reused nor destroyed) until the
+ * signal shows it ended.  After RTC_ETIMEDOUT the caller must not free, reuse or unregister either buffer while
+ * rtc_dma_pending over it is > 0; rtc_host_unregister refuses such a range with RTC_EBUSY.
+ * rtc_dma_pending: the number of listed copies whose source or destination overlaps [p, p + bytes) (p = NULL: all),
+ * reaping those that have ended. */
+int rtc_dma_pending(const void *p, size_t bytes);
+/* Test hook of that bookkeeping (no copy engine involved): list (pending != 0) or drop a simulated in-flight copy
+ * into [p, p + bytes). */
+int rtc_dma_debug_inflight(void *p, size_t bytes, int pending);
 /* Copy `rows` rows of `rowBytes` from device memory (row pitch srcPitch) into page-locked host memory (row pitch
  * hostPitch) with the SDMA engines, blocking until done: one SDMA sub-window copy (all pointers, pitches and rowBytes
  * multiples of 4), else one linear copy per row.  A rank's compact rows y = r + k*G (rtc_render_rows_async with
@@ -234,6 +247,14 @@ typedef struct RtcLoopStats {
 int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d,
                    void *const *devRows, void *const *hostRows, size_t hostPitch, int nbuf, int frames, void *stream,
                    RtcLoopStats *stats);
+/* The same loop with a moving camera: frame k renders with cams[k % ncams] (e.g. an orbit; every camera change
+ * re-derives the per-launch primary records, and an unjoined sky pass of another camera is waited for before the
+ * next launch writes its buffer).  rtc_frame_loop is this with ncams = 1.  On an error (e.g. RTC_ETIMEDOUT from a
+ * copy) the loop stops enqueueing, waits for the copies it started and returns the first error; no buffer is
+ * rendered into again after its copy failed. */
+int rtc_frame_loop_cameras(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cams, int ncams,
+                           const RtcRenderDesc *d, void *const *devRows, void *const *hostRows, size_t hostPitch,
+                           int nbuf, int frames, void *stream, RtcLoopStats *stats);
 
 /* Re-assemble a row-interleaved gather: dCompact holds `parts` blocks of rowsPerPart*width*3 bytes, block
  * g holding rows y = g + k*parts; dOut receives the height*width*3 frame.  Asynchronous on `stream`. */

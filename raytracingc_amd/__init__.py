@@ -34,6 +34,8 @@ from ._abi import (  # noqa: F401
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
     RTC_SEGMENT_COUNTERS,
+    RTC_EBUSY,
+    RTC_ETIMEDOUT,
     SCENE_DT,
     SPHERE_DT,
     TRIANGLE_DT,
@@ -246,11 +248,12 @@ class DeviceScene:
         check(lib().rtc_scene_set_frame_event(self._h, C.c_void_p(event_handle) if event_handle else None),
               "rtc_scene_set_frame_event")
 
-    def frame_loop(self, scene: Scene, cam: RtcCamera, cfg: RenderConfig, dev_rows: list, host_rows: list,
+    def frame_loop(self, scene: Scene, cam, cfg: RenderConfig, dev_rows: list, host_rows: list,
                    host_pitch: int, frames: int, stream: int | None = None) -> dict:
         """rtc_frame_loop: `frames` pipelined frames of cfg's rows, rendered into the device buffers dev_rows[k % n]
         and copied (SDMA, native copy thread) into the page-locked host buffers host_rows[k % n] with row pitch
-        host_pitch; returns when the last frame is in host memory."""
+        host_pitch; returns when the last frame is in host memory.  `cam` is one RtcCamera, or a sequence of them:
+        frame k then renders with cam[k % len(cam)] (rtc_frame_loop_cameras, a moving camera)."""
         n = len(dev_rows)
         if len(host_rows) != n:
             raise ValueError("frame_loop: one host buffer per device buffer")
@@ -258,9 +261,15 @@ class DeviceScene:
         dv = (C.c_void_p * n)(*dev_rows)
         hv = (C.c_void_p * n)(*host_rows)
         st = RtcLoopStats()
-        check(lib().rtc_frame_loop(self._h, C.byref(scene), C.byref(cam), C.byref(d), dv, hv, C.c_size_t(host_pitch),
-                                   n, int(frames), C.c_void_p(stream) if stream else None, C.byref(st)),
-              "rtc_frame_loop")
+        strm = C.c_void_p(stream) if stream else None
+        if isinstance(cam, RtcCamera):
+            check(lib().rtc_frame_loop(self._h, C.byref(scene), C.byref(cam), C.byref(d), dv, hv,
+                                       C.c_size_t(host_pitch), n, int(frames), strm, C.byref(st)), "rtc_frame_loop")
+        else:
+            cams = (RtcCamera * len(cam))(*cam)
+            check(lib().rtc_frame_loop_cameras(self._h, C.byref(scene), cams, len(cam), C.byref(d), dv, hv,
+                                               C.c_size_t(host_pitch), n, int(frames), strm, C.byref(st)),
+                  "rtc_frame_loop_cameras")
         return {"wall_ms": st.wallMs, "frames": st.frames, "enqueue_ms": st.enqueueMs,
                 "copy_ms_median": st.copyMsMedian, "copy_ms_max": st.copyMsMax}
 
@@ -306,7 +315,17 @@ def host_register(ptr: int, nbytes: int) -> None:
 
 
 def host_unregister(ptr: int) -> None:
+    """rtc_host_unregister; raises RtcError(RTC_EBUSY) while a timed-out copy may still write the range."""
     check(lib().rtc_host_unregister(C.c_void_p(ptr)), "rtc_host_unregister")
+
+
+def dma_pending(ptr: int | None = None, nbytes: int = 0) -> int:
+    """rtc_dma_pending: copies that timed out (RTC_ETIMEDOUT) and may still read or write [ptr, ptr + nbytes)
+    (None: any range).  Buffers they touch must not be freed or reused while this is > 0."""
+    n = lib().rtc_dma_pending(C.c_void_p(ptr) if ptr else None, C.c_size_t(nbytes if ptr else 0))
+    if n < 0:
+        check(n, "rtc_dma_pending")
+    return n
 
 
 def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# RTC_LIB_PATH selects the diagnostic build (librtc_diag.so) for tools/kernel_probe.py only
+# RTC_LIB_PATH selects another build of the library (e.g. the diagnostic librtc_diag.so for tools/chain_sections.py)
 LIB_PATH = os.environ.get("RTC_LIB_PATH") or os.path.join(HERE, "_lib", "librtc.so")
 CLI_PATH = os.path.join(HERE, "_lib", "rtc")
 
@@ -102,6 +102,7 @@ RTC_F_OVERLAP = 0x800
 RTC_F_HOST_ROWS = 0x1000
 RTC_SEGMENT_COUNTERS = 5  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005
+RTC_ETIMEDOUT, RTC_EBUSY = -10006, -10007
 
 assert C.sizeof(Vec3) == 12 and C.sizeof(Scene) == 56 and C.sizeof(Material) == 20
 assert C.sizeof(Sphere) == 36 and C.sizeof(Triangle) == 68 and C.sizeof(Ray) == 24
@@ -136,7 +137,7 @@ EXPORTS = [
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
     "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
-    "rtc_host_unregister", "rtc_frame_loop",
+    "rtc_host_unregister", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
 ]
@@ -196,6 +197,10 @@ def lib() -> C.CDLL:
     L.rtc_host_unregister.argtypes = [vp]
     L.rtc_frame_loop.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp, sz, ip,
                                  ip, vp, C.POINTER(RtcLoopStats)]
+    L.rtc_frame_loop_cameras.argtypes = [vp, C.POINTER(Scene), vp, ip, C.POINTER(RtcRenderDesc), vp, vp, sz, ip, ip,
+                                         ip, vp, C.POINTER(RtcLoopStats)]
+    L.rtc_dma_pending.argtypes = [vp, sz]
+    L.rtc_dma_debug_inflight.argtypes = [vp, sz, ip]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]
     L.rtc_render_rows_async.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp,
                                         vp, vp]

@@ -575,10 +575,45 @@ struct DmaSignal {
     }
 };
 
-/* wait until `sig` drops below 1; RTC_EIO when the copy reports an error (negative value) or has not completed
- * after 20 s (a faulted or lost copy must not hang the caller) */
-int dma_wait(hsa_signal_t sig, const char *what)
+/* Copies that did not complete within the wait limit (dma_wait): the engine may still read [srcLo, srcHi) and write
+ * [dstLo, dstHi) and decrement `sig`.  They stay listed -- their signal neither reused nor destroyed -- until the signal
+ * shows the copy ended (rtc_dma_pending reaps them); rtc_host_unregister refuses a range one of them may still write.
+ * `simulated` entries (rtc_dma_debug_inflight, CPU tests of this bookkeeping) have no signal. */
+struct InflightCopy {
+    uintptr_t dstLo, dstHi, srcLo, srcHi;
+    hsa_signal_t sig;
+};
+std::mutex g_inflightMu;
+std::vector<InflightCopy> g_inflight;
+
+/* copies still pending whose destination or source overlaps [lo, hi); finished ones are reaped */
+int inflight_overlapping(uintptr_t lo, uintptr_t hi)
 {
+    std::lock_guard<std::mutex> lk(g_inflightMu);
+    int n = 0;
+    for (size_t i = 0; i < g_inflight.size();) {
+        InflightCopy &c = g_inflight[i];
+        if (c.sig.handle && hsa_signal_load_scacquire(c.sig) < 1) { /* completed (0) or failed (< 0): engine done */
+            (void)hsa_signal_destroy(c.sig);
+            g_inflight.erase(g_inflight.begin() + (ptrdiff_t)i);
+            continue;
+        }
+        n += (c.dstLo < hi && lo < c.dstHi) || (c.srcLo < hi && lo < c.srcHi);
+        ++i;
+    }
+    return n;
+}
+
+/* wait until the thread's copy signal drops below 1; RTC_EIO when the copy reports an error (negative value).  After
+ * the wait limit (20 s, RTC_DMA_TIMEOUT_MS) a faulted or lost copy must not hang the caller, but the engine may still
+ * write: the copy is listed in flight with its signal (the thread takes a fresh one for its next copy) and
+ * RTC_ETIMEDOUT tells the caller not to free, reuse or unregister dst / src until rtc_dma_pending says it ended. */
+int dma_wait(hsa_signal_t &sig, const void *dst, size_t dstBytes, const void *src, size_t srcBytes, const char *what)
+{
+    static const double limitMs = [] {
+        const char *e = getenv("RTC_DMA_TIMEOUT_MS");
+        return e && atof(e) > 0.0 ? atof(e) : 20000.0;
+    }();
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 1000000,
@@ -587,8 +622,16 @@ int dma_wait(hsa_signal_t sig, const char *what)
             return 0;
         if (v < 0)
             return rtc_fail(RTC_EIO, "%s: the copy engine reported an error (signal %lld)", what, (long long)v);
-        if (ms_since(t0) > 20000.0)
-            return rtc_fail(RTC_EIO, "%s: copy not completed after 20 s", what);
+        if (ms_since(t0) > limitMs) {
+            {
+                std::lock_guard<std::mutex> lk(g_inflightMu);
+                g_inflight.push_back(InflightCopy{(uintptr_t)dst, (uintptr_t)dst + dstBytes, (uintptr_t)src,
+                                                  (uintptr_t)src + srcBytes, sig});
+            }
+            sig.handle = 0; /* owned by the in-flight list now */
+            return rtc_fail(RTC_ETIMEDOUT, "%s: copy not completed after %.0f ms; it may still write its destination "
+                                           "(rtc_dma_pending)", what, limitMs);
+        }
     }
 }
 
@@ -644,7 +687,7 @@ extern "C" int rtc_copy_d2h_dma(void *hostDst, const void *devSrc, size_t bytes)
     hsa_signal_store_screlease(sig.s, 1);
     if (hsa_amd_memory_async_copy(dst, cpu, devSrc, gpu, bytes, 0, nullptr, sig.s) != HSA_STATUS_SUCCESS)
         return rtc_fail(RTC_EIO, "rtc_copy_d2h_dma: hsa_amd_memory_async_copy failed");
-    return dma_wait(sig.s, "rtc_copy_d2h_dma");
+    return dma_wait(sig.s, hostDst, bytes, devSrc, bytes, "rtc_copy_d2h_dma");
 }
 
 extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void *devSrc, size_t srcPitch,
@@ -655,7 +698,7 @@ extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void
         return rtc_fail(RTC_EINVAL, "rtc_copy_rows_d2h_dma: bad argument");
     if (rows == 0 || rowBytes == 0)
         return 0;
-    const size_t span = (size_t)(rows - 1) * hostPitch + rowBytes;
+    const size_t span = (size_t)(rows - 1) * hostPitch + rowBytes, srcSpan = (size_t)(rows - 1) * srcPitch + rowBytes;
     hsa_agent_t gpu, cpu;
     void *dst = nullptr;
     if (int rc = dma_endpoints(hostDst, span, devSrc, "rtc_copy_rows_d2h_dma", gpu, dst, cpu))
@@ -686,11 +729,11 @@ extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void
             if (hsa_amd_memory_async_copy((char *)dst + (size_t)r * hostPitch, cpu, (const char *)devSrc + (size_t)r * srcPitch,
                                           gpu, rowBytes, 0, nullptr, sig.s) != HSA_STATUS_SUCCESS) {
                 hsa_signal_subtract_screlease(sig.s, rows - r); /* the copies not issued */
-                (void)dma_wait(sig.s, "rtc_copy_rows_d2h_dma");
+                (void)dma_wait(sig.s, hostDst, span, devSrc, srcSpan, "rtc_copy_rows_d2h_dma");
                 return rtc_fail(RTC_EIO, "rtc_copy_rows_d2h_dma: hsa_amd_memory_async_copy failed (row %d)", r);
             }
     }
-    return dma_wait(sig.s, "rtc_copy_rows_d2h_dma");
+    return dma_wait(sig.s, hostDst, span, devSrc, srcSpan, "rtc_copy_rows_d2h_dma");
 }
 
 /* Page-locked through the HSA runtime itself (hsa_amd_memory_lock for every agent), so the range has the LOCKED
@@ -714,6 +757,15 @@ extern "C" int rtc_host_unregister(void *p)
 {
     if (!p)
         return rtc_fail(RTC_EINVAL, "rtc_host_unregister: null pointer");
+    size_t bytes = 1;
+    {
+        std::lock_guard<std::mutex> lk(g_lockedMu);
+        auto it = g_locked.find((uintptr_t)p);
+        if (it != g_locked.end())
+            bytes = it->second.bytes;
+    }
+    if (const int n = inflight_overlapping((uintptr_t)p, (uintptr_t)p + bytes))
+        return rtc_fail(RTC_EBUSY, "rtc_host_unregister: %d timed-out copies may still write this range", n);
     {
         std::lock_guard<std::mutex> lk(g_lockedMu);
         g_locked.erase((uintptr_t)p);
@@ -721,6 +773,31 @@ extern "C" int rtc_host_unregister(void *p)
     if (hsa_amd_memory_unlock(p) != HSA_STATUS_SUCCESS)
         return rtc_fail(RTC_EIO, "rtc_host_unregister: hsa_amd_memory_unlock failed");
     return 0;
+}
+
+extern "C" int rtc_dma_pending(const void *p, size_t bytes)
+{
+    if (!p && bytes)
+        return rtc_fail(RTC_EINVAL, "rtc_dma_pending: null pointer");
+    return p ? inflight_overlapping((uintptr_t)p, (uintptr_t)p + (bytes ? bytes : 1))
+             : inflight_overlapping(0, ~(uintptr_t)0);
+}
+
+extern "C" int rtc_dma_debug_inflight(void *p, size_t bytes, int pending)
+{
+    if (!p || !bytes)
+        return rtc_fail(RTC_EINVAL, "rtc_dma_debug_inflight: empty range");
+    std::lock_guard<std::mutex> lk(g_inflightMu);
+    if (pending) {
+        g_inflight.push_back(InflightCopy{(uintptr_t)p, (uintptr_t)p + bytes, 0, 0, hsa_signal_t{0}});
+        return 0;
+    }
+    for (size_t i = 0; i < g_inflight.size(); ++i)
+        if (!g_inflight[i].sig.handle && g_inflight[i].dstLo == (uintptr_t)p && g_inflight[i].dstHi == (uintptr_t)p + bytes) {
+            g_inflight.erase(g_inflight.begin() + (ptrdiff_t)i);
+            return 0;
+        }
+    return rtc_fail(RTC_EINVAL, "rtc_dma_debug_inflight: no simulated copy for this range");
 }
 
 /* ---- pipelined frames (the host frame loop) -------------------------------------------------------------------
@@ -732,11 +809,11 @@ extern "C" int rtc_host_unregister(void *p)
  * finished.  The reference's equivalent is main.c:285-305: the threads write their rows into the shared image, which
  * stbi_write_bmp then reads. */
 
-extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d,
-                              void *const *devRows, void *const *hostRows, size_t hostPitch, int nbuf, int frames,
-                              void *stream, RtcLoopStats *stats)
+extern "C" int rtc_frame_loop_cameras(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cams, int ncams,
+                                      const RtcRenderDesc *d, void *const *devRows, void *const *hostRows,
+                                      size_t hostPitch, int nbuf, int frames, void *stream, RtcLoopStats *stats)
 {
-    if (!s || !scene || !cam || !d || !devRows || !hostRows || nbuf <= 0 || nbuf > 16 || frames < 0)
+    if (!s || !scene || !cams || ncams <= 0 || !d || !devRows || !hostRows || nbuf <= 0 || nbuf > 16 || frames < 0)
         return rtc_fail(RTC_EINVAL, "rtc_frame_loop: bad argument");
     for (int b = 0; b < nbuf; ++b)
         if (!devRows[b] || !hostRows[b])
@@ -811,7 +888,7 @@ extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCa
         const auto e0 = std::chrono::steady_clock::now();
         rc = rtc_scene_set_frame_event(s, ready[b]);
         if (!rc)
-            rc = rtc_render_rows_async(s, scene, cam, &dd, devRows[b], nullptr, nullptr, stream);
+            rc = rtc_render_rows_async(s, scene, &cams[k % ncams], &dd, devRows[b], nullptr, nullptr, stream);
         enqueueMs += ms_since(e0);
         if (!rc) {
             std::lock_guard<std::mutex> lk(m);
@@ -825,6 +902,7 @@ extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCa
         cv.notify_all();
     }
     copier.join();
+    (void)rtc_scene_set_frame_event(s, nullptr); /* never leave ready[] armed: it is destroyed on return */
     const double wall = ms_since(t0);
     if (!rc && err)
         rc = rtc_fail(err, "%s", errMsg.c_str());
@@ -842,4 +920,13 @@ extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCa
         stats->copyMsMax = copyMs.empty() ? 0.0 : copyMs.back();
     }
     return rc;
+}
+
+extern "C" int rtc_frame_loop(RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d,
+                              void *const *devRows, void *const *hostRows, size_t hostPitch, int nbuf, int frames,
+                              void *stream, RtcLoopStats *stats)
+{
+    if (!cam)
+        return rtc_fail(RTC_EINVAL, "rtc_frame_loop: bad argument");
+    return rtc_frame_loop_cameras(s, scene, cam, 1, d, devRows, hostRows, hostPitch, nbuf, frames, stream, stats);
 }

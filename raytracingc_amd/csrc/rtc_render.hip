@@ -154,7 +154,11 @@ struct __attribute__((aligned(32))) DevCluster {
 constexpr unsigned kOrderEventFlags = hipEventDisableTiming | (RTC_ORDER_FENCE ? 0u : hipEventDisableSystemFence);
 /* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
 constexpr int kSkySlots = 8;
-constexpr int kGeoRing = 16, kGeoSetInts = 16 * 32; /* kGeoLists counters, 32 ints apart */
+/* rtc_render_chain's geometry-pixel sub-lists: kGeoLists counters, kGeoCountStride ints (one 128-B line) apart; a ring
+ * of kGeoRing counter sets of kGeoSetInts ints (see RtcDeviceScene::geoCounts) */
+constexpr int kGeoLists = 16, kGeoCountStride = 32;
+constexpr int kGeoRing = 16, kGeoSetInts = kGeoLists * kGeoCountStride;
+static_assert(kGeoSetInts >= kGeoLists * kGeoCountStride, "a counter set holds every sub-list counter");
 struct SkyKey {
     const void *colors, *accum;
     float cam[13], env[14];
@@ -660,7 +664,6 @@ template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
 #endif
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
-constexpr int kGeoLists = 16, kGeoCountStride = 32; /* ints: one 128-B line per counter */
 
 
 /* The pixel a lane renders and its primary ray (rowThread, main.c:88-94).  A 256-thread workgroup covers
@@ -1275,7 +1278,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         if (lane == 0)
             base = atomicAdd(&P.geoCount[l * kGeoCountStride], __popcll(b));
         base = __builtin_amdgcn_readfirstlane(base);
-        if ((b >> lane) & 1ull)
+        /* a sub-list holds every geometry pixel of its tiles (geoCap = 64 x its tiles) when its counter started at 0;
+         * a stale counter must not write past it (the readers clamp the counts to geoCap too) */
+        if (((b >> lane) & 1ull) && base + __popcll(b) <= P.geoCap)
             P.geoList[(size_t)l * P.geoCap + base + __popcll(b & ((1ull << lane) - 1ull))] = tile * 64 + lane;
     }
     if (lane == 0 && b)
@@ -2042,7 +2047,7 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 {
     int items = 0;
     for (int l = 0; l < kGeoLists; ++l)
-        items += P.geoCount[l * kGeoCountStride];
+        items += min(P.geoCount[l * kGeoCountStride], P.geoCap);
     items = min(items, P.sampleCap);
     for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
         const SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
@@ -2175,7 +2180,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     /* the sub-lists' inclusive prefix counts, lane l < kGeoLists holding sub-list l's, loaded once per wave: an
      * item's sub-list is then a ballot, not a chain of dependent count loads as a wave's items pass the sub-lists */
-    int incl = lane < kGeoLists ? P.geoCount[lane * kGeoCountStride] : 0;
+    int incl = lane < kGeoLists ? min(P.geoCount[lane * kGeoCountStride], P.geoCap) : 0;
 #pragma unroll
     for (int d = 1; d < kGeoLists; d <<= 1) {
         const int v = __shfl_up(incl, d);
@@ -2492,7 +2497,16 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                      const RtcRenderDesc *d, void *dColors, float *dAccum,
                                      unsigned long long *dSegments, void *stream)
 {
-    if (!s || !scene || !cam || !d || !dColors)
+    if (!s)
+        return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: null scene");
+    RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
+    /* The hooks are one-shot: this launch takes the events armed before it and forgets them -- before any early
+     * return, so a later launch never records an event its caller has since released (rtc_scene_set_geometry_event /
+     * _frame_event); a launch that fails records neither */
+    const hipEvent_t geoEvent = s->geoEvent, frameEvent = s->frameEvent;
+    ms->geoEvent = nullptr;
+    ms->frameEvent = nullptr;
+    if (!scene || !cam || !d || !dColors)
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: null argument");
     if (d->width <= 0 || d->height <= 0 || d->rowStride <= 0 || d->rowStart < 0)
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: bad geometry %dx%d rows %d+k*%d", d->width, d->height,
@@ -2503,12 +2517,16 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_COOP4 / COOP8 / PIPE / SPEC name kernels that were "
                                     "removed (rtc_render_chain renders every geometry pixel)");
     const int rows = rtc_rows_selected(d);
-    if (rows == 0)
-        return 0;
     /* the scene's buffers, scratch and kernels live on s->device; the caller's current device is restored */
     RtcDeviceGuard guard(s->device);
     if (!guard.ok())
         return rtc_fail(RTC_ENODEV, "rtc_render_rows_async: cannot select the scene's device %d", s->device);
+    if (rows == 0) { /* nothing to render: the (empty) frame is complete once `stream` gets here */
+        for (hipEvent_t ev : {geoEvent, frameEvent})
+            if (ev)
+                HIP_TRY(hipEventRecord(ev, (hipStream_t)stream));
+        return 0;
+    }
     RenderParams P;
     memset(&P, 0, sizeof P);
     P.tris = s->tris;
@@ -2563,13 +2581,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
      * that counts segments joins, the reduction reads the sky kernel's counters) */
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
-    RtcDeviceScene *const ms = const_cast<RtcDeviceScene *>(s);
     const int half = overlap ? s->flip : 0; /* the scratch slot this launch writes */
-    /* The hooks are one-shot: this launch records the events armed before it and forgets them, so a later launch
-     * never records an event its caller has since released (rtc_scene_set_geometry_event / _frame_event). */
-    const hipEvent_t geoEvent = s->geoEvent, frameEvent = s->frameEvent;
-    ms->geoEvent = nullptr;
-    ms->frameEvent = nullptr;
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
      * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
@@ -2660,7 +2672,12 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const float org[3] = {P.origin.x, P.origin.y, P.origin.z};
     const bool prepCurrent = s->prepValid && s->prepStream == st && memcmp(s->prepOrigin, org, sizeof org) == 0;
     const bool countsZeroed = !chain || (s->cullValid && s->cullStream == st);
+    /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
+     * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
+    if (chain)
+        ms->cullValid = false;
     if ((s->triPadded > 0 || chain) && !(prepCurrent && countsZeroed)) {
+        ms->prepValid = false;
         hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
                            s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin,
                            chain ? P.geoCount : nullptr);
@@ -2669,15 +2686,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         ms->prepStream = st;
         memcpy(ms->prepOrigin, org, sizeof org);
     }
-    if (chain) {
-        ms->geoSeq++;
-        ms->cullValid = true;
-        ms->cullStream = st;
-    }
     if (cull) {
         /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
         HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st,
                             fused && RTC_SIDE_STREAM ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
+        if (chain) { /* this cull zeroes the next set's counters (P.geoCountNext) on `st` */
+            ms->geoSeq++;
+            ms->cullValid = true;
+            ms->cullStream = st;
+        }
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {

@@ -83,3 +83,56 @@ def test_flag_constants_match_header():
             assert getattr(abi, name) == int(val, 0), name
     for name in [n for n in found if n.startswith("RTC_F_")]:
         assert hasattr(abi, name), f"{name} missing from raytracingc_amd/_abi.py"
+
+
+def test_dma_timeout_bookkeeping():
+    """an SDMA copy that times out may still write its destination.  The library lists it (here a
+    simulated one, rtc_dma_debug_inflight: no copy engine needed) until it ends: rtc_dma_pending counts the listed
+    copies overlapping a range, rtc_host_unregister refuses such a range with RTC_EBUSY, and the entry is dropped once
+    the copy is known to have ended (include/rtc.h, RTC_ETIMEDOUT contract)."""
+    L = rt.lib()
+    buf = (C.c_ubyte * 4096)()
+    p = C.addressof(buf)
+    assert rt.dma_pending(p, 4096) == 0
+    assert L.rtc_dma_debug_inflight(C.c_void_p(p + 1024), 512, 1) == 0
+    try:
+        assert rt.dma_pending(p, 4096) == 1
+        assert rt.dma_pending(p, 1024) == 0  # [p, p + 1024) ends where the copy's range starts
+        assert rt.dma_pending(p + 1535, 1) == 1 and rt.dma_pending(p + 1536, 64) == 0
+        assert rt.dma_pending(None) >= 1
+        assert L.rtc_host_unregister(C.c_void_p(p + 1024)) == _abi.RTC_EBUSY
+        assert b"timed-out" in L.rtc_last_error()
+        with pytest.raises(rt.RtcError) as ei:
+            rt.host_unregister(p + 1024)
+        assert ei.value.code == _abi.RTC_EBUSY
+    finally:
+        assert L.rtc_dma_debug_inflight(C.c_void_p(p + 1024), 512, 0) == 0
+    assert rt.dma_pending(p, 4096) == 0
+    # dropping a copy that is not listed, or an empty range, is an argument error
+    assert L.rtc_dma_debug_inflight(C.c_void_p(p), 512, 0) == _abi.RTC_EINVAL
+    assert L.rtc_dma_debug_inflight(None, 0, 1) == _abi.RTC_EINVAL
+    assert L.rtc_dma_pending(None, 16) == _abi.RTC_EINVAL
+
+
+def test_bench_orbit_cameras():
+    """bench.py's moving-camera leg: distinct origins at the default camera's distance and height, all looking at
+    the default point (main.c:252-255 bases), the middle of the sweep near the default camera."""
+    import math
+    import sys
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    cams = bench.orbit_cameras(rt)
+    assert len(cams) == bench.ORBIT_FRAMES
+    origins = {(c.origin.x, c.origin.y, c.origin.z) for c in cams}
+    assert len(origins) == len(cams)
+    lx, ly, lz = rt.DEFAULT_LOOKING_AT
+    ox, oy, oz = rt.DEFAULT_ORIGIN
+    r0 = math.hypot(ox - lx, oz - lz)
+    for c in cams:
+        assert abs(c.origin.y - oy) < 1e-6 and abs(math.hypot(c.origin.x - lx, c.origin.z - lz) - r0) < 1e-4
+        # ez is the unit vector towards the look-at point
+        d = (lx - c.origin.x, ly - c.origin.y, lz - c.origin.z)
+        n = math.sqrt(sum(v * v for v in d))
+        assert abs(c.ez.x - d[0] / n) < 1e-5 and abs(c.ez.z - d[2] / n) < 1e-5

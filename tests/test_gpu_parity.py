@@ -840,3 +840,143 @@ def test_frame_loop_pipelined_host_frames(gpu_available):
         del frames, shm
         mm.close()
     ds.close()
+
+
+@pytest.mark.parametrize("scene,spp,G", [("complex", 64, 4), ("ultracomplex", 64, 8), ("ultracomplex", 256, 8)])
+def test_4k_row_shares_assemble_bit_exact(scene, spp, G, gpu_available):
+    """BASELINE.json C4 (complex 3840x2160x64 over 4 GPUs), NS (ultracomplex 4K x64) and C5 (ultracomplex 4K x256)
+    over 8 GPUs: every rank's share (rows y = r + k*G, main.c:84 lifted to GPUs; 540 / 270 rows of 3840, so the
+    deferred-sum path with 8x8 tiles spanning 32-64 image rows) rendered on one device, assembled two ways -- the
+    RCCL path's re-interleave on the device (rtc_deinterleave_async) and the host-frame path's strided SDMA copies
+    into one pinned frame (rtc_copy_rows_d2h_dma) -- equals the single-GPU 4K frame bit for bit, bytes and floats;
+    the last share equals the oracle's render of the same rows (rowStart, rowStride) bit for bit with the same
+    paths; and the pipelined per-rank frame loop the bench runs (rtc_frame_loop, RTC_F_OVERLAP) builds the same
+    host frame."""
+    import torch
+
+    from raytracingc_amd.distributed import rows_per_rank
+
+    tris, tonly = load_tris(scene)
+    sc, cam, _ = setup_from_flags({})
+    W, H = 3840, 2160
+    ref, racc, _ = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True), want_accum=True)
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.current_stream().cuda_stream
+    rows = rows_per_rank(H, G)
+    parts = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
+    accs = torch.zeros((G, rows, W, 3), dtype=torch.float32, device="cuda")
+    for r in range(G):
+        cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
+        assert cfg.rows() * W > 400000  # not a small share: deferred sums (rtc_accumulate_samples)
+        ds.render_rows_async(sc, cam, cfg, parts[r].data_ptr(), accs[r].data_ptr(), None, st)
+    out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    rt.deinterleave_async(parts.data_ptr(), G, rows, W, H, out.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref), "device re-interleave"
+    pinned = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True)
+    for r in range(G):
+        rt.copy_rows_d2h_dma(pinned.data_ptr() + r * W * 3, G * W * 3, parts[r].data_ptr(), W * 3, W * 3,
+                             len(range(r, H, G)))
+    assert np.array_equal(pinned.numpy(), ref), "strided SDMA host frame"
+    a = accs.cpu().numpy()
+    for r in range(G):
+        n = len(range(r, H, G))
+        assert np.array_equal(_bits(a[r, :n]), _bits(racc[r::G])), f"rank {r} floats"
+    # the pipelined per-rank loop of bench.py, every rank's frames into one pinned host frame pair
+    host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    dev = [torch.zeros((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    lst = torch.cuda.Stream()
+    for r in range(G):
+        cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
+        ds.frame_loop(sc, cam, cfg, [d.data_ptr() for d in dev], [h.data_ptr() + r * W * 3 for h in host], G * W * 3,
+                      3, lst.cuda_stream)
+    for h in host:
+        assert np.array_equal(h.numpy(), ref), "frame loop host frame"
+    ds.close()
+    r0 = G - 1
+    ocol, oacc, oseg = orc.render(tris, None, sc, cam, RtcRenderDesc(W, H, spp, 10, tonly, r0, G, 0), threads=16)
+    n = len(range(r0, H, G))
+    assert np.array_equal(_bits(a[r0, :n]), _bits(oacc)) and np.array_equal(parts[r0, :n].cpu().numpy(), ocol)
+    _, _, sr = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True, row_start=r0, row_stride=G))
+    assert sr["segments"] == oseg
+
+
+def test_prep_skip_across_streams(gpu_available):
+    """rtc_prep_primary is skipped when the camera origin and the stream are those of the previous split
+    launch, whose tile cull zeroed this launch's sub-list counters.  Same origin on streams A, B, A, A (joined and
+    pipelined), then a camera change and back: every frame equals rtc_render bit for bit."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene = rt.default_scene()
+    cam, cam2 = rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1)
+    W, H, spp = 256, 144, 8
+    ref = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))[0]
+    ref2 = rt.render(tris, None, scene, cam2, rt.RenderConfig(W, H, spp, 10, True))[0]
+    ds = rt.DeviceScene(tris, None)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for overlap in (False, True):
+        cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=overlap)
+        for s, c, want in ((sa, cam, ref), (sb, cam, ref), (sa, cam, ref), (sa, cam, ref), (sa, cam2, ref2),
+                           (sb, cam2, ref2), (sa, cam, ref)):
+            buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+            ev = torch.cuda.Event()
+            ev.record(s)
+            ds.set_frame_event(ev.cuda_event)
+            ds.render_rows_async(scene, c, cfg, buf.data_ptr(), stream=s.cuda_stream)
+            ev.synchronize()
+            assert np.array_equal(buf.cpu().numpy(), want), overlap
+    torch.cuda.synchronize()
+    ds.close()
+
+
+def test_moving_camera_frame_loop(gpu_available):
+    """rtc_frame_loop_cameras (the bench's moving-camera leg): frame k renders with camera k mod 5 into buffer
+    k mod 3; each host buffer holds the last frame written into it, equal to rtc_render of that frame's camera."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene = rt.default_scene()
+    cams = [rt.camera_basis((-4.75 + 0.3 * k, -1.5 - 0.05 * k, -4.75 + 0.2 * k), rt.DEFAULT_LOOKING_AT, 1.0)
+            for k in range(5)]
+    W, H, spp, frames = 320, 180, 8, 7
+    refs = [rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))[0] for c in cams]
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    dev = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(3)]
+    out = ds.frame_loop(scene, cams, rt.RenderConfig(W, H, spp, 10, True), [d.data_ptr() for d in dev],
+                        [h.data_ptr() for h in host], W * 3, frames, st.cuda_stream)
+    assert out["frames"] == frames
+    for b in range(3):
+        k = max(k for k in range(frames) if k % 3 == b)
+        assert np.array_equal(host[b].numpy(), refs[k % 5]), f"buffer {b} (frame {k})"
+    ds.close()
+
+
+def test_empty_launch_consumes_frame_event(gpu_available):
+    """a launch that selects no rows returns at once but still takes (and records) the armed one-shot
+    events, so the next launch cannot record an event its caller released after the empty one."""
+    import torch
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, spp = 160, 90, 4
+    ref = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))[0]
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    ev = torch.cuda.Event()
+    ev.record(st)
+    ds.set_frame_event(ev.cuda_event)
+    ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, spp, 10, True, row_start=H), buf.data_ptr(),
+                         stream=st.cuda_stream)
+    ev.synchronize()
+    del ev
+    torch.cuda.synchronize()
+    for overlap in (False, True):
+        ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, spp, 10, True, overlap=overlap), buf.data_ptr(),
+                             stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), ref)
+    ds.close()
