@@ -198,7 +198,7 @@ def lib() -> C.CDLL:
     L.rtc_frame_loop.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp, sz, ip,
                                  ip, vp, C.POINTER(RtcLoopStats)]
     L.rtc_frame_loop_cameras.argtypes = [vp, C.POINTER(Scene), vp, ip, C.POINTER(RtcRenderDesc), vp, vp, sz, ip, ip,
-                                         ip, vp, C.POINTER(RtcLoopStats)]
+                                         vp, C.POINTER(RtcLoopStats)]
     L.rtc_dma_pending.argtypes = [vp, sz]
     L.rtc_dma_debug_inflight.argtypes = [vp, sz, ip]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]

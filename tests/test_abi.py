@@ -136,3 +136,19 @@ def test_bench_orbit_cameras():
         d = (lx - c.origin.x, ly - c.origin.y, lz - c.origin.z)
         n = math.sqrt(sum(v * v for v in d))
         assert abs(c.ez.x - d[0] / n) < 1e-5 and abs(c.ez.z - d[2] / n) < 1e-5
+
+
+def test_ctypes_signatures_match_header():
+    """Every argtypes list of the ctypes mirror has as many entries as the header's prototype has parameters."""
+    txt = open(os.path.join(REPO, "include", "rtc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    L = rt.lib()
+    checked = 0
+    for name, params in re.findall(r"\b(rtc_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", txt):
+        params = params.strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        at = getattr(L, name).argtypes
+        if at is not None:
+            assert len(at) == n, f"{name}: {len(at)} argtypes, header declares {n} parameters"
+            checked += 1
+    assert checked >= 25
