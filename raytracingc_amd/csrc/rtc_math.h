@@ -425,8 +425,31 @@ RTC_HD float powf_glibc_pos(float x, float y, const double (*log2tab)[2] = powf_
 #include "rtc_bm_tables.h"
 
 constexpr double kBmLn2Hi = 6.93147180369123816490e-01, kBmLn2Lo = 1.90821492927058770002e-10; /* 43-bit hi */
-constexpr double kBmRhoTol = 0x1p-46; /* relative to rho */
+constexpr double kBmRhoTol = 0x1p-44; /* relative to rho */
 constexpr double kBmNrmTol = 0x1p-46; /* absolute, per unit rho */
+
+/* f32 sqrt for the Newton seed of bm_rho_d: v_sqrt_f32 on the device (<= 1 ulp for the normal arguments it gets
+ * here), the correctly rounded sqrtf on the host -- the seed's error enters only through the Newton step's bound */
+RTC_HD float bm_sqrtf(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+/* 1 / x for x in [2^-125, 2^125] (rtc_device.h rcp_cr: v_rcp_f32 and two FMA Newton steps, the IEEE quotient for every
+ * such x), inf for x = 0 */
+RTC_HD float bm_rcpf(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r = __builtin_amdgcn_rcpf(x);
+    r = __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+#else
+    return 1.0f / x;
+#endif
+}
 
 /* half an ulp of a normal float f (exponent field E >= 1), as a double */
 RTC_HD double bm_half_ulp(float f) { return u2d((unsigned long long)(((f2u(f) >> 23) & 0xffu) + 1023u - 151u) << 52); }
@@ -439,8 +462,10 @@ RTC_HD double bm_rho_d(float u, const BmLogEntry *logTab = kBmLogTab)
     const BmLogEntry e = logTab[(tmp >> 16) & 127u];
     const double dk = (double)((int)tmp >> 23);
     const double r = fma((double)u2f(iu - (tmp & 0xff800000u)), (double)e.invc, -1.0); /* exact */
-    double q = 1.0 / 7.0; /* log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6 + r^5/7) */
-    q = fma(q, r, -1.0 / 6.0);
+    /* log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6): the dropped r^7/7 is below 2^-51.8 absolute (|r| <=
+     * 2^-7 in the entry of c = 1), the largest relative error of rho it leaves is 1.7e-14 = 2^-45.8 (at u = 1 - 2^-7,
+     * exhaustive over every float u, tools/check_devmath.cpp), inside kBmRhoTol = 2^-44 */
+    double q = -1.0 / 6.0;
     q = fma(q, r, 0.2);
     q = fma(q, r, -0.25);
     q = fma(q, r, 1.0 / 3.0);
@@ -448,7 +473,17 @@ RTC_HD double bm_rho_d(float u, const BmLogEntry *logTab = kBmLogTab)
     const double p = fma(r * r, q, r);
     const double hi = fma(dk, kBmLn2Hi, e.logcHi);
     const double lo = fma(dk, kBmLn2Lo, (double)e.logcLo) + p;
-    return __builtin_sqrt(-2.0 * (hi + lo));
+    const double L = -2.0 * (hi + lo);
+    /* sqrt(L) without the correctly rounded double square root: the f32 root of (float)L, rf = sqrt(L) (1 + d) with
+     * |d| <= 2^-23 + 2^-25 (the rounding of L, v_sqrt_f32's ulp), and one Newton step in double, rho = rf + (L - rf^2)
+     * / (2 rf), its quotient from the correctly rounded f32 1 / (2 rf): the step leaves d^2 / 2 < 2^-46.6 and the
+     * quotient's error |d| 2^-24 < 2^-46.7 of rho, together inside kBmRhoTol = 2^-44 (every float u is checked on the
+     * GPU, tools/exact_probe.hip).  L >= 2^-23 for u < 1 (the RNG's u are >= 2^-32, so L < 45); u = 1 gives L = 0: rf
+     * = 0, its 1 / rf inf and rho NaN -- not certified (bm_rho_fast) */
+    const float rf = bm_sqrtf((float)L);
+    const double e2 = fma(-(double)rf, (double)rf, L);
+    const float hq = 0.5f * bm_rcpf(rf);
+    return fma(e2, (double)hq, (double)rf);
 }
 /* rho = (float)sqrt(-2 log((double)u)) for u in (0, 1]; false: not certified (use the exact path) */
 RTC_HD bool bm_rho_fast(float u, float &rho, const BmLogEntry *logTab = kBmLogTab)
@@ -467,13 +502,13 @@ RTC_HD double bm_cos_d(float theta, const double (*cosTab)[2] = kBmCosTab)
     double t = fma(-jd, kBmStepHi, th); /* exact */
     t = fma(-jd, kBmStepLo, t);
     const double z = t * t;
-    double c = 1.0 / 40320.0; /* cos t = 1 - z/2 + z^2/24 - z^3/720 + z^4/40320 */
-    c = fma(c, z, -1.0 / 720.0);
+    /* z = t^2 <= 2^-8.7: cos t = 1 - z/2 + z^2/24 - z^3/720 (the dropped z^4/8! < 2^-50), sin t = t (1 - z/6 + z^2/120 -
+     * z^3/5040) (the dropped t z^4/9! < 2^-57) */
+    double c = -1.0 / 720.0;
     c = fma(c, z, 1.0 / 24.0);
     c = fma(c, z, -0.5);
     c = fma(c, z, 1.0);
-    double sn = 1.0 / 362880.0; /* sin t = t (1 - z/6 + z^2/120 - z^3/5040 + z^4/362880) */
-    sn = fma(sn, z, -1.0 / 5040.0);
+    double sn = -1.0 / 5040.0;
     sn = fma(sn, z, 1.0 / 120.0);
     sn = fma(sn, z, -1.0 / 6.0);
     sn = fma(sn * z, t, t);

@@ -606,6 +606,10 @@ struct RenderParams {
     const unsigned long long *__restrict__ pixMask;  /* per 8x8 tile: pixels with a primary candidate (bit i =
                                                        pixel i, row-major); the others see only the sky */
     const int *__restrict__ order; /* null: identity; else launch slot -> workgroup (heavy first) */
+    /* rtc_super_cull's survivors (maskWords u64 per superblock of kSuperBlocks x kSuperBlocks workgroup blocks,
+     * superX per row of superblocks); null: rtc_tile_cull tests every triangle at level 1 */
+    const unsigned long long *__restrict__ superMask;
+    int superX;
     /* rtc_render_chain's work: kGeoLists sub-lists of geometry pixels (tile*64 + bit), filled by rtc_tile_cull
      * (tile t appends to sub-list t % kGeoLists, one atomic per tile with geometry, spread over kGeoLists
      * counters in separate cache lines); geoCount[l * 32] = entries of sub-list l, zeroed by the previous split
@@ -1194,6 +1198,31 @@ __device__ bool tile_prunes(const TileCone &K, const DevPrimF &F)
     return false;
 }
 
+/* Level 0 of the tile cull: the same prefilter over a superblock of kSuperBlocks x kSuperBlocks workgroup blocks (64 x 64
+ * pixels of the launch's rows), one wave each.  A triangle it prunes fails the filter for every pixel of the superblock,
+ * so rtc_tile_cull's level 1 tests only its survivors, and a block whose superblock keeps none (the sky of a frame)
+ * skips its own double-precision cone.  Same candidate lists bit for bit (each level only removes triangles the
+ * per-pixel filter rejects for every pixel of the rectangle). */
+#ifndef RTC_CULL_SUPER
+#define RTC_CULL_SUPER 1
+#endif
+constexpr int kSuperBlocks = 4;
+constexpr size_t kSuperCullPixels = 400000; /* launches of more pixels run level 0 */
+__global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned long long *__restrict__ superMask)
+{
+    const int sx = blockIdx.x, sy = blockIdx.y, lane = threadIdx.x;
+    const int x0 = sx * kSuperBlocks * kTileW, r0 = sy * kSuperBlocks * kTileH;
+    const TileCone K = rect_cone(P, x0, x0 + kSuperBlocks * kTileW - 1, r0, r0 + kSuperBlocks * kTileH - 1);
+    unsigned long long *out = superMask + (size_t)(sy * P.superX + sx) * P.maskWords;
+    for (int w = 0; w < P.maskWords; ++w) {
+        const int ti = w * 64 + lane;
+        const bool maybe = ti < P.triPadded && (!K.ok || !tile_prunes(K, P.primF[ti]));
+        const unsigned long long m = __ballot(maybe);
+        if (lane == 0)
+            out[w] = m;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
                                                        unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
                                                        unsigned long long *__restrict__ pixMask)
@@ -1214,11 +1243,19 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     /* level 1: the prefilter over the workgroup's 16x16 pixels (a superset of each tile's direction range, so
      * a triangle it prunes fails for every pixel of the four tiles); the waves share the mask words */
     __syncthreads();
-    if (wave < P.maskWords) { /* wave-uniform: only the waves with mask words need the block's cone */
+    /* the superblock's survivors (level 0, rtc_super_cull; all ones without it): wave-uniform scalar loads */
+    const unsigned long long *sup =
+        P.superMask ? P.superMask + (size_t)((by / kSuperBlocks) * P.superX + bx / kSuperBlocks) * P.maskWords : nullptr;
+    bool supAny = !sup;
+    for (int w = 0; sup && w < P.maskWords && !supAny; ++w)
+        supAny = KCONST(sup)[w] != 0ull;
+    if (wave < P.maskWords && supAny) { /* wave-uniform: only the waves with mask words need the block's cone */
         const TileCone KB = rect_cone(P, bx * kTileW, bx * kTileW + kTileW - 1, by * kTileH, by * kTileH + kTileH - 1);
         for (int w = wave; w < P.maskWords; w += kBlock / 64) {
             const int ti = w * 64 + lane;
-            const bool maybe = ti < P.triPadded && (!RTC_TILE_PREFILTER || !KB.ok || !tile_prunes(KB, P.primF[ti]));
+            const unsigned long long sw = sup ? KCONST(sup)[w] : ~0ull;
+            const bool maybe = ((sw >> lane) & 1ull) && ti < P.triPadded &&
+                               (!RTC_TILE_PREFILTER || !KB.ok || !tile_prunes(KB, P.primF[ti]));
             const unsigned long long m = __ballot(maybe);
             if (lane == 0) {
                 sBlockCand[w] = m;
@@ -1667,7 +1704,11 @@ __device__ __forceinline__ void wave_lds_sync()
 /* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile of a 16x16 block; the waves of
  * tiles whose pixels all have primary candidates return at once (rtc_render_chain renders those).  Few registers, so many
  * waves per SIMD hide the latency of the environment's double-precision chains. */
-__global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const unsigned *__restrict__ tileW)
+#ifndef RTC_SKY_WAVES
+#define RTC_SKY_WAVES 8 /* <= 64 VGPRs: two sky workgroups fit where one chain workgroup retires (frame -1.5 %, round 4) */
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky(
+    RenderParams P, const unsigned *__restrict__ tileW)
 {
     __shared__ PowTablesLds sPow;
     __shared__ __attribute__((aligned(4))) unsigned char sSkyRow[kBlock / 64][8][24];
@@ -1697,7 +1738,11 @@ __global__ __launch_bounds__(kBlock) void rtc_render_sky(RenderParams P, const u
             } else {
 #pragma unroll RTC_SKY_UNROLL
                 for (int s = 0; s < P.spp; ++s) {
+#ifdef RTC_AB_CHEAP_ENV_SKY /* timing experiment only (the sky pass's environment cost) */
+                    const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(px.dir.y + (float)s * 1e-9f, 0.f));
+#else
                     const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
+#endif
                     acc = add(acc, mul(l, P.invSpp));
                 }
             }
@@ -2304,7 +2349,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         DSECT_END(dc2, 2);
                     } else {
                         DSECT_BEGIN(dc6);
+#ifdef RTC_AB_CHEAP_ENV_CHAIN /* timing experiment only (the environment's cost in the chain kernel) */
+                        light = add(light, mulv(lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y, 0.f)), rayColor));
+#else
                         light = add(light, mulv(environment(dir, P.env), rayColor)); /* raytracing.c:291 */
+#endif
                         endSample = true;
                         DSECT_END(dc6, 6);
                     }
@@ -2342,8 +2391,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 const int take = min(q - p, P.spp - k);
                 /* a run of one-hit samples: j advances by 1 */
                 if (deferred) {
+#ifndef RTC_AB_NO_SLOTS /* timing experiment only (the deferred slots' cost): nothing stored, no sum pass */
                     if (lane >= p && lane < p + take)
                         slot[k + lane - p] = SampleSlot{t.x, t.y, t.z};
+#endif
                 } else {
                     if (lane >= p && lane < p + take) {
                         const int i = staged + lane - p;
@@ -2490,6 +2541,11 @@ __host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
 #ifndef RTC_SIDE_STREAM
 #define RTC_SIDE_STREAM 1
 #endif
+#ifdef RTC_AB_NO_SLOTS
+#define RTC_AB_NO_SLOTS_ON 1
+#else
+#define RTC_AB_NO_SLOTS_ON 0
+#endif
 #ifndef RTC_CHAIN_PRIMF
 #define RTC_CHAIN_PRIMF 1 /* stage the primary filter records in LDS when the block's budget allows */
 #endif
@@ -2577,6 +2633,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const bool fused = cull && !debug && P.sphereCount == 0 && !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
+    const dim3 superGrid((grid.x + kSuperBlocks - 1) / kSuperBlocks, (grid.y + kSuperBlocks - 1) / kSuperBlocks);
+    const size_t superBytes = RTC_CULL_SUPER ? (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long) : 0;
     const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64);
     /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
      * that counts segments joins, the reduction reads the sky kernel's counters) */
@@ -2606,7 +2664,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     size_t halfBytes = 0;
     if (cull) {
         const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + blocks + 4) * sizeof(int) +
-                            (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int); /* + sub-lists */
+                            (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int) + /* + sub-lists */
+                            8 + superBytes; /* + the superblock survivors (8-byte aligned) */
         halfBytes = (need + 255) & ~(size_t)255;
         if (kSkySlots * halfBytes > s->scratchCap) { /* every slot (hipFree synchronises the device: no pass reads them) */
             if (ms->scratch)
@@ -2637,6 +2696,12 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
     unsigned *tileW = cull ? weight + blocks : nullptr;
     int *order = cull ? (int *)(tileW + tiles) : nullptr;
+    unsigned long long *superMask = nullptr;
+    if (cull && superBytes) { /* after the sub-lists, 8-byte aligned */
+        const size_t off = ((size_t)((const unsigned char *)(order + blocks + 4 + kGeoLists * kGeoCountStride +
+                                                             (size_t)kGeoLists * geoCap) - s->scratch) + 7) & ~(size_t)7;
+        superMask = (unsigned long long *)(s->scratch + off);
+    }
     if (chain) {
         P.geoCount = s->geoCounts + (size_t)(s->geoSeq % kGeoRing) * kGeoSetInts;
         P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
@@ -2686,6 +2751,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         ms->prepStream = st;
         memcpy(ms->prepOrigin, org, sizeof org);
     }
+    /* level 0 pays for its extra launch on large frames only (1080p: -7 us per frame); a small share (the 1/8 of a
+     * row-partitioned 1080p frame) culls faster without it (round 4 A/B: 0.111 vs 0.118 ms per joined share) */
+    const bool superCull = (size_t)d->width * (size_t)rows > kSuperCullPixels;
+    if (cull && superMask && superCull && s->maskWords > 0) {
+        P.superMask = superMask;
+        P.superX = (int)superGrid.x;
+        hipLaunchKernelGGL(rtc_super_cull, superGrid, dim3(64), 0, st, P, superMask);
+        HIP_TRY(hipGetLastError());
+    }
     if (cull) {
         /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
         HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st,
@@ -2732,7 +2806,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const size_t dyn = rec + (P.chainPrimF ? pf : 0);
             /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
-            hipEvent_t chainStop = overlap && P.sampleCap == 0 ? s->evGeoDone : nullptr;
+            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone : nullptr;
             const dim3 cg(kChainWorkers), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, st, chainStop, P));
@@ -2744,7 +2818,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, st, chainStop, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
-            if (P.sampleCap > 0) {
+            if (P.sampleCap > 0 && !RTC_AB_NO_SLOTS_ON) {
                 const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
                 HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, overlap ? s->evGeoDone : nullptr, P));
                 HIP_TRY(hipGetLastError());
