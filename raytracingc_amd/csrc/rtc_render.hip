@@ -1075,6 +1075,63 @@ __device__ __forceinline__ Closest closest_hit(const RenderParams &P, V3 pos, V3
     return c;
 }
 
+#ifdef RTC_DIAG
+/* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp, cycles inside
+ * closest_hit} */
+__device__ unsigned long long *g_rtc_diag = nullptr;
+extern "C" int rtc_diag_set_buffer(void *dptr)
+{
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_diag), &dptr, sizeof dptr));
+    return 0;
+}
+/* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
+ * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
+__device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
+/* rtc_tile_cull stamps, summed over waves: [0] start .. level 1 done, [1] level 1 done .. end (sky blocks), [2] level-2
+ * prefilter, [3] per-pixel candidate loop, [4] list append .. end, [5] sky-block waves, [6] geometry-block waves, [7]
+ * candidates looped over (per wave) */
+__device__ unsigned long long g_rtc_cull[12]; /* [8] geometry waves: level 1 done .. pixel loops done, [9] whole */
+extern "C" int rtc_diag_cull(unsigned long long *out12, int reset)
+{
+    if (out12)
+        HIP_TRY(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_rtc_cull), 12 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[12] = {0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_cull), z, sizeof z));
+    }
+    return 0;
+}
+#define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define CADD(k, val)                                                                                           \
+    do {                                                                                                       \
+        if ((threadIdx.x & 63) == 0)                                                                           \
+            atomicAdd(&g_rtc_cull[k], (unsigned long long)(val));                                              \
+    } while (0)
+__shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..15 (rtc_render_chain) */
+#define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DSECT_END(v, k)                                                                                        \
+    do {                                                                                                       \
+        const unsigned long long dsectNow = __builtin_amdgcn_s_memtime();                                      \
+        if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))                           \
+            s_rtc_sect[threadIdx.x >> 6][k] += dsectNow - (v);                                                 \
+    } while (0)
+extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
+{
+    if (out8)
+        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 16 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
+    }
+    return 0;
+}
+#else
+#define DSECT_BEGIN(v) (void)0
+#define DSECT_END(v, k) (void)0
+#define CSTAMP(v) (void)0
+#define CADD(k, val) (void)0
+#endif
+
 /* Tile candidate lists for primary segments.  A pixel's primary ray is the same ray for every sample
  * (main.c:88-94: no jitter), so the primary filter's verdict for (pixel, triangle) is the same for
  * every sample.  One pass over the launch's pixels records, per 8x8 tile (= one wave of the render kernel),
@@ -1229,6 +1286,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 {
     __shared__ unsigned wgWeight, wgAny;
     extern __shared__ unsigned long long sBlockCand[]; /* maskWords: the block's 16x16 prefilter survivors */
+    CSTAMP(c0);
     if (threadIdx.x == 0) {
         wgWeight = 0;
         wgAny = 0;
@@ -1265,6 +1323,8 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         }
     }
     __syncthreads();
+    CSTAMP(c1);
+    CADD(0, c1 - c0);
     const int tile = wave_tile(bx, by);
     unsigned long long *out = mask + (size_t)tile * P.maskWords;
     if (!wgAny) { /* workgroup-uniform: no triangle survives for any of its pixels (most of a sky-heavy frame) */
@@ -1276,8 +1336,15 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         }
         if (threadIdx.x == 0)
             weight[blockIdx.y * gridDim.x + blockIdx.x] = 0u;
+        CSTAMP(c9);
+        CADD(1, c9 - c1);
+        CADD(5, 1);
         return;
     }
+    CADD(6, 1);
+#ifdef RTC_DIAG
+    unsigned long long dPre = 0, dLoop = 0, dCand = 0;
+#endif
     const PixelRay px = pixel_ray(P, bx, by);
     bool anyCand = false;
     /* level 2: the tile's own prefilter on the block's survivors, then the per-pixel filter */
@@ -1286,9 +1353,15 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         /* lane l: may triangle 64w + l pass for some pixel of the tile? */
         const int ti = w * 64 + lane;
         const unsigned long long bc = sBlockCand[w];
+        CSTAMP(c2);
         const bool maybe = ((bc >> lane) & 1ull) && (!RTC_TILE_PREFILTER || !K.ok || !tile_prunes(K, P.primF[ti]));
         unsigned long long todo = bc ? __ballot(maybe) : 0ull;
         unsigned long long bits = 0;
+        CSTAMP(c3);
+#ifdef RTC_DIAG
+        dPre += c3 - c2;
+        dCand += (unsigned long long)__popcll(todo);
+#endif
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -1298,9 +1371,19 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
             if (__ballot(keep))
                 bits |= 1ull << j;
         }
+        CSTAMP(c4);
+#ifdef RTC_DIAG
+        dLoop += c4 - c3;
+#endif
         if (lane == 0)
             out[w] = bits;
     }
+    CSTAMP(c5);
+#ifdef RTC_DIAG
+    CADD(2, dPre);
+    CADD(3, dLoop);
+    CADD(7, dCand);
+#endif
     /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
      * non-empty candidate list exactly when its weight is > 0 */
     const unsigned long long b = __ballot(anyCand);
@@ -1325,6 +1408,10 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     __syncthreads();
     if (threadIdx.x == 0)
         weight[blockIdx.y * gridDim.x + blockIdx.x] = wgWeight;
+    CSTAMP(c6);
+    CADD(4, c6 - c5);
+    CADD(8, c5 - c1);
+    CADD(9, c6 - c0);
 }
 
 /* Launch order of the render kernel's workgroups: a counting sort of the weights, heaviest bucket first
@@ -1413,40 +1500,6 @@ __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(unsigned long l
     }
 }
 
-#ifdef RTC_DIAG
-/* diagnostic build only (librtc_diag.so): per-wave {cycles, wave-loop iterations, start stamp, cycles inside
- * closest_hit} */
-__device__ unsigned long long *g_rtc_diag = nullptr;
-extern "C" int rtc_diag_set_buffer(void *dptr)
-{
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_diag), &dptr, sizeof dptr));
-    return 0;
-}
-/* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
- * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
-__device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
-__shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..15 (rtc_render_chain) */
-#define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define DSECT_END(v, k)                                                                                        \
-    do {                                                                                                       \
-        const unsigned long long dsectNow = __builtin_amdgcn_s_memtime();                                      \
-        if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))                           \
-            s_rtc_sect[threadIdx.x >> 6][k] += dsectNow - (v);                                                 \
-    } while (0)
-extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
-{
-    if (out8)
-        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 16 * sizeof(unsigned long long)));
-    if (reset) {
-        unsigned long long z[16] = {0};
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
-    }
-    return 0;
-}
-#else
-#define DSECT_BEGIN(v) (void)0
-#define DSECT_END(v, k) (void)0
-#endif
 
 #ifndef RTC_MIN_WAVES
 #define RTC_MIN_WAVES 1
@@ -1854,6 +1907,12 @@ constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * s
 #define RTC_CHAIN_WGS_PER_CU 4
 #endif
 constexpr size_t kChainLdsBudget = 160 * 1024 / RTC_CHAIN_WGS_PER_CU;
+#ifndef RTC_CHAIN_LDS_MIN
+#define RTC_CHAIN_LDS_MIN 0
+#endif
+#ifndef RTC_INLINE_ALL
+#define RTC_INLINE_ALL 0 /* every launch sums in-kernel (A/B) */
+#endif
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records; the owner's ray
  * by ds_bpermute from the owner lane (every lane takes part), the exact-safe filter, the reference arithmetic for
@@ -2713,7 +2772,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
          * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
          * 4K 1/8 share are faster deferred) */
         const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
-        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare) {
+        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !RTC_INLINE_ALL) {
             const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
@@ -2803,7 +2862,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const size_t rec = s->chunkCount <= 1 ? (size_t)s->clusterCount * kClusterSize * sizeof(DevTri) : 0;
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
             P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kChainLdsBudget;
-            const size_t dyn = rec + (P.chainPrimF ? pf : 0);
+            /* RTC_CHAIN_LDS_MIN: a floor on the block's LDS, to cap the chain workgroups per CU (co-residence
+             * experiments: 3 per CU leave a quarter of every SIMD's registers to the sky pass) */
+            const size_t dyn = std::max<size_t>(rec + (P.chainPrimF ? pf : 0),
+                                                RTC_CHAIN_LDS_MIN > kChainStaticLds ? RTC_CHAIN_LDS_MIN - kChainStaticLds : 0);
             /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
             hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone : nullptr;
