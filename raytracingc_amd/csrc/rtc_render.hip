@@ -166,6 +166,7 @@ struct SkyKey {
 };
 struct RtcDeviceScene {
     int device;
+    int cuCount; /* compute units of the device (the persistent chain kernel's workgroups are a multiple of it) */
     int triCount, triPadded, sphereCount; /* triPadded: multiple of kUnroll, zero (never-hit) records */
     int clusterCount;   /* ceil(triCount / kClusterSize) */
     DevTri *clTris;     /* clusterCount * kClusterSize records in cluster order, pad0 = reference index (int) */
@@ -461,6 +462,10 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         ct.assign(1, DevTri{});
     RtcDeviceScene *s = new RtcDeviceScene();
     s->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256; /* MI355X */
+    s->cuCount = cus;
     s->triCount = triCount;
     s->triPadded = (triCount + 7) / 8 * 8; /* whole pairs of batches; arrays hold 8 more records for prefetch */
     s->sphereCount = sphereCount;
@@ -1863,10 +1868,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
 constexpr size_t kInlineSumPixels = 400000;          /* shares (row stride > 1) up to this many pixels sum in-kernel */
 constexpr int kChainBlock = 256;
-#ifndef RTC_CHAIN_WORKERS
-#define RTC_CHAIN_WORKERS 1024 /* = the resident capacity (4 workgroups per CU): no second round of workgroups */
+/* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
+ * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
+ * in the chain kernel's idle issue slots instead of waiting for its tail, and the launch stream's small kernels are no
+ * longer starved by that tail (round 4: frame 0.372 -> 0.351 ms).  A small share of a row-partitioned frame runs 4 (its
+ * chain kernel is the critical path).  Workers = per-CU count x CUs: exactly the resident capacity, no second round. */
+#ifndef RTC_CHAIN_WGS_FULL
+#define RTC_CHAIN_WGS_FULL 3
 #endif
-constexpr int kChainWorkers = RTC_CHAIN_WORKERS;
+#ifndef RTC_CHAIN_WGS_SHARE
+#define RTC_CHAIN_WGS_SHARE 4
+#endif
 #ifndef RTC_CHAIN_UNROLL
 #define RTC_CHAIN_UNROLL 2
 #endif
@@ -1903,15 +1915,11 @@ static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a fu
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
 constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
-#ifndef RTC_CHAIN_WGS_PER_CU
-#define RTC_CHAIN_WGS_PER_CU 4
-#endif
-constexpr size_t kChainLdsBudget = 160 * 1024 / RTC_CHAIN_WGS_PER_CU;
-#ifndef RTC_CHAIN_LDS_MIN
-#define RTC_CHAIN_LDS_MIN 0
-#endif
+constexpr size_t kCuLds = 160 * 1024; /* gfx950 LDS per CU */
+/* the block LDS that keeps the chain workgroups per CU at most n: above kCuLds / (n + 1) */
+constexpr size_t chain_lds_floor(int n) { return n >= 4 ? 0 : kCuLds / (size_t)(n + 1) + 256; }
 #ifndef RTC_INLINE_ALL
-#define RTC_INLINE_ALL 0 /* every launch sums in-kernel (A/B) */
+#define RTC_INLINE_ALL 0 /* every launch sums in-kernel */
 #endif
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records; the owner's ray
@@ -2761,6 +2769,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                                              (size_t)kGeoLists * geoCap) - s->scratch) + 7) & ~(size_t)7;
         superMask = (unsigned long long *)(s->scratch + off);
     }
+    /* a small share of a row-partitioned frame (the 1080p frame's 1/8): its chain kernel is the critical path */
+    const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
     if (chain) {
         P.geoCount = s->geoCounts + (size_t)(s->geoSeq % kGeoRing) * kGeoSetInts;
         P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
@@ -2771,7 +2781,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
          * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
          * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
          * 4K 1/8 share are faster deferred) */
-        const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
         if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !RTC_INLINE_ALL) {
             const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
@@ -2859,17 +2868,17 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evHeavy0, st));
             /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
              * filter records when the block stays within 4 per CU */
+            const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : RTC_CHAIN_WGS_FULL;
             const size_t rec = s->chunkCount <= 1 ? (size_t)s->clusterCount * kClusterSize * sizeof(DevTri) : 0;
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
-            P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kChainLdsBudget;
-            /* RTC_CHAIN_LDS_MIN: a floor on the block's LDS, to cap the chain workgroups per CU (co-residence
-             * experiments: 3 per CU leave a quarter of every SIMD's registers to the sky pass) */
+            P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;
+            const size_t floorLds = chain_lds_floor(wgsPerCu);
             const size_t dyn = std::max<size_t>(rec + (P.chainPrimF ? pf : 0),
-                                                RTC_CHAIN_LDS_MIN > kChainStaticLds ? RTC_CHAIN_LDS_MIN - kChainStaticLds : 0);
+                                                floorLds > kChainStaticLds ? floorLds - kChainStaticLds : 0);
             /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
             hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone : nullptr;
-            const dim3 cg(kChainWorkers), cb(kChainBlock);
+            const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, st, chainStop, P));
             else if (s->chunkCount > 1)
