@@ -280,7 +280,13 @@ __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
     float skyGradientT = 0.f;
     /* smoothstep's value is +0 .. 1 or NaN (never negative, never -0: clamp01 keeps -0 but (-0)^2 = +0) and the
      * exponent 0.35 is not special, so glibc's powf takes its positive-x path: that path alone, branch-free */
-    if (__any(__float_as_uint(skyArg) != 0u))
+    const unsigned sa = __float_as_uint(skyArg);
+#ifndef RTC_SKY_UNIT
+#define RTC_SKY_UNIT 1
+#endif
+    if (RTC_SKY_UNIT && __all(sa - 0x00800000u <= 0x3f800000u - 0x00800000u)) /* every lane normal x in (0, 1]: main path */
+        skyGradientT = s.log2tab ? rtcmath::powf_sky_unit(skyArg, s.log2tab, s.exp2tab) : rtcmath::powf_sky_unit(skyArg);
+    else if (__any(sa != 0u))
         skyGradientT = s.log2tab ? rtcmath::powf_glibc_pos<true>(skyArg, 0.35f, s.log2tab, s.exp2tab)
                                  : rtcmath::powf_glibc_pos<true>(skyArg, 0.35f);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);

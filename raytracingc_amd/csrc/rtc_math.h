@@ -410,6 +410,17 @@ RTC_HD float powf_glibc_pos(float x, float y, const double (*log2tab)[2] = powf_
     return r;
 }
 
+/* getEnvironmentLight's sky term powf(x, 0.35f) (raytracing.c:153) for a normal x in [2^-126, 1] (smoothstep's value
+ * above the horizon): glibc's main path alone.  There 0.35 log2(x) lies in [-44.1, 0], so none of powf_glibc_pos's
+ * special results (x = 0, inf, NaN, subnormal x, the exp2 step's overflow and underflow limits) applies and its selects
+ * are no-ops.  Bit-identical to powf_glibc(x, 0.35f) on every such x (tools/exact_probe.hip). */
+RTC_HD float powf_sky_unit(float x, const double (*log2tab)[2] = powf_data::kLog2Tab,
+                           const unsigned long long *exp2tab = powf_data::kExp2Tab)
+{
+    const double logx = powf_log2<true>(f2u(x), log2tab);
+    return powf_exp2<true>((double)0.35f * logx, 0u, exp2tab);
+}
+
 /* ---- certified fast Box-Muller (RandomValueNormalDistrubtion, moremath.c:97-102) -----------------------
  * The reference's rho = (float)sqrt(-2 log(u)) and n = (float)((double)rho * cos((double)theta)) need glibc's
  * log and cos only up to the final float rounding.  The fast path evaluates them with short table-driven

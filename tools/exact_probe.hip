@@ -2,7 +2,8 @@
 // all 2^32 float bit patterns (test infrastructure; tests/test_gpu_exact.py runs it, `make probe` builds it):
 //   sqrt_cr(x)  == (float)sqrt((double)x)        (length(), moremath.c:9)
 //   rcp_cr(x)   == 1.f / x  (IEEE f32 divide)     (normalized(), moremath.c:14; (float)(1./x) == 1.f/x)
-//   powf_glibc_pos(x, y) == powf_glibc(x, y) bit for bit, every x with the sign bit clear, y in kPowY
+//   powf_glibc_pos(x, y) == powf_glibc(x, y) bit for bit, every x with the sign bit clear, y in kPowY;
+//   powf_sky_unit(x) == powf_glibc(x, 0.35f), every normal x in [2^-126, 1]
 //                                                 (getEnvironmentLight's powf, raytracing.c:153,155)
 //   bm_rho_fast(u) == (float)sqrt(-2 log u) (exact restatement) whenever certified, every float u in (0, 1];
 //   bm_normal_fast(rho, theta) == (float)(rho cos theta) likewise, every float theta in [0, 2 pi] x 4 rho
@@ -59,6 +60,11 @@ __global__ void check_pow(unsigned long long base, unsigned long long *bad)
     const unsigned long long m = __ballot(b != 0);
     if ((threadIdx.x & 63) == 0 && m)
         atomicAdd(&bad[2], (unsigned long long)__popcll(m));
+    const bool unit = i >= 0x00800000ull && i <= 0x3f800000ull &&
+                      __float_as_uint(rtcmath::powf_sky_unit(x)) != __float_as_uint(rtcmath::powf_glibc<true>(x, 0.35f));
+    const unsigned long long mu = __ballot(unit);
+    if ((threadIdx.x & 63) == 0 && mu)
+        atomicAdd(&bad[6], (unsigned long long)__popcll(mu));
 }
 
 __device__ __forceinline__ float smoothstep_div(float inf, float sup, float x)
@@ -116,11 +122,11 @@ __global__ void check_bm(unsigned long long base, unsigned long long *bad)
 int main()
 {
     unsigned long long *bad;
-    if (hipMalloc(&bad, 6 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&bad, 7 * sizeof(unsigned long long)) != hipSuccess) {
         printf("no device\n");
         return 2;
     }
-    (void)hipMemset(bad, 0, 6 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 7 * sizeof(unsigned long long));
     const unsigned long long chunk = 1ull << 30;
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
@@ -130,7 +136,7 @@ int main()
         hipLaunchKernelGGL(check_bm, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
     for (unsigned long long base = 0; base < (1ull << 32); base += chunk)
         hipLaunchKernelGGL(check_smooth, dim3((unsigned)(chunk / 256)), dim3(256), 0, nullptr, base, bad);
-    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
         printf("copy failed\n");
         return 2;
@@ -141,5 +147,6 @@ int main()
     printf("smoothstep_sky mismatches %llu checked %llu\n", h[3], 1ull << 32);
     printf("smoothstep_ground mismatches %llu checked %llu\n", h[4], 1ull << 32);
     printf("bm_fast mismatches %llu checked %llu\n", h[5], 0x3f800000ull + 4 * 0x40c90fdcull);
-    return (h[0] | h[1] | h[2] | h[3] | h[4] | h[5]) ? 1 : 0;
+    printf("powf_sky_unit mismatches %llu checked %llu\n", h[6], 0x3f800000ull - 0x00800000ull + 1);
+    return (h[0] | h[1] | h[2] | h[3] | h[4] | h[5] | h[6]) ? 1 : 0;
 }
