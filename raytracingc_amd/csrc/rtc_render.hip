@@ -1092,25 +1092,21 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 /* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
 __device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
-/* rtc_tile_cull stamps, summed over waves: [0] start .. level 1 done, [1] level 1 done .. end (sky blocks), [2] level-2
- * prefilter, [3] per-pixel candidate loop, [4] list append .. end, [5] sky-block waves, [6] geometry-block waves, [7]
- * candidates looped over (per wave) */
-__device__ unsigned long long g_rtc_cull[12]; /* [8] geometry waves: level 1 done .. pixel loops done, [9] whole */
-extern "C" int rtc_diag_cull(unsigned long long *out12, int reset)
+#define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+/* per-block records of rtc_tile_cull (wave 0): {start, level 1 done, end, geometry, level-2 prefilter cycles, candidate
+ * loop cycles, candidates, 0}, written with plain stores into the buffer rtc_diag_set_cull_buffer names (null: none) */
+__device__ unsigned long long *g_rtc_cullwg = nullptr;
+extern "C" int rtc_diag_set_cull_buffer(void *dptr)
 {
-    if (out12)
-        HIP_TRY(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_rtc_cull), 12 * sizeof(unsigned long long)));
-    if (reset) {
-        unsigned long long z[12] = {0};
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_cull), z, sizeof z));
-    }
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_cullwg), &dptr, sizeof dptr));
     return 0;
 }
-#define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define CADD(k, val)                                                                                           \
+#define CREC(blk, a, b, c, geo, pre, loop, cand)                                                              \
     do {                                                                                                       \
-        if ((threadIdx.x & 63) == 0)                                                                           \
-            atomicAdd(&g_rtc_cull[k], (unsigned long long)(val));                                              \
+        if (g_rtc_cullwg && threadIdx.x == 0) {                                                                \
+            unsigned long long *r_ = g_rtc_cullwg + (size_t)(blk) * 8;                                         \
+            r_[0] = (a), r_[1] = (b), r_[2] = (c), r_[3] = (geo), r_[4] = (pre), r_[5] = (loop), r_[6] = (cand); \
+        }                                                                                                      \
     } while (0)
 __shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..15 (rtc_render_chain) */
 #define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -1134,7 +1130,7 @@ extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
 #define DSECT_BEGIN(v) (void)0
 #define DSECT_END(v, k) (void)0
 #define CSTAMP(v) (void)0
-#define CADD(k, val) (void)0
+#define CREC(blk, a, b, c, geo, pre, loop, cand) (void)0
 #endif
 
 /* Tile candidate lists for primary segments.  A pixel's primary ray is the same ray for every sample
@@ -1329,7 +1325,6 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     }
     __syncthreads();
     CSTAMP(c1);
-    CADD(0, c1 - c0);
     const int tile = wave_tile(bx, by);
     unsigned long long *out = mask + (size_t)tile * P.maskWords;
     if (!wgAny) { /* workgroup-uniform: no triangle survives for any of its pixels (most of a sky-heavy frame) */
@@ -1342,11 +1337,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         if (threadIdx.x == 0)
             weight[blockIdx.y * gridDim.x + blockIdx.x] = 0u;
         CSTAMP(c9);
-        CADD(1, c9 - c1);
-        CADD(5, 1);
+        CREC(blockIdx.y * gridDim.x + blockIdx.x, c0, c1, c9, 0, 0, 0, 0);
         return;
     }
-    CADD(6, 1);
 #ifdef RTC_DIAG
     unsigned long long dPre = 0, dLoop = 0, dCand = 0;
 #endif
@@ -1383,12 +1376,6 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         if (lane == 0)
             out[w] = bits;
     }
-    CSTAMP(c5);
-#ifdef RTC_DIAG
-    CADD(2, dPre);
-    CADD(3, dLoop);
-    CADD(7, dCand);
-#endif
     /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
      * non-empty candidate list exactly when its weight is > 0 */
     const unsigned long long b = __ballot(anyCand);
@@ -1414,9 +1401,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     if (threadIdx.x == 0)
         weight[blockIdx.y * gridDim.x + blockIdx.x] = wgWeight;
     CSTAMP(c6);
-    CADD(4, c6 - c5);
-    CADD(8, c5 - c1);
-    CADD(9, c6 - c0);
+#ifdef RTC_DIAG
+    CREC(blockIdx.y * gridDim.x + blockIdx.x, c0, c1, c6, 1, dPre, dLoop, dCand);
+#endif
 }
 
 /* Launch order of the render kernel's workgroups: a counting sort of the weights, heaviest bucket first
