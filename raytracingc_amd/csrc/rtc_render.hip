@@ -176,8 +176,12 @@ struct RtcDeviceScene {
     DevTri *tris;
     DevMat *mats;
     DevSphere *spheres;
-    DevPrimF *primF; /* per-launch scratch, written by rtc_prep_primary on the launch stream */
+    /* per-launch primary records, one copy per scratch slot (primStride records each), written by rtc_prep_primary:
+     * an overlapped launch's preparation (on the cull stream) may run while the previous frame's geometry kernel still
+     * reads its own copy */
+    DevPrimF *primF;
     DevPrimX *primX;
+    size_t primStride;
     /* per-launch scratch (rtc_tile_cull / rtc_order_blocks): the candidate bit-sets (maskWords u64 per 8x8
      * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
     unsigned char *scratch;
@@ -193,13 +197,20 @@ struct RtcDeviceScene {
     unsigned long long geoSeq;
     hipStream_t cullStream;
     bool cullValid;
-    /* rtc_prep_primary's records are for prepOrigin, written on prepStream (prepValid: they exist) */
-    bool prepValid;
-    float prepOrigin[3];
-    hipStream_t prepStream;
+    /* rtc_prep_primary's records of slot h are for prepOrigin[h], written on prepStream[h] (prepValid[h]: they exist) */
+    bool prepValid[kSkySlots];
+    float prepOrigin[kSkySlots][3];
+    hipStream_t prepStream[kSkySlots];
+    /* RTC_F_OVERLAP launches prepare and cull on `cst` (a high-priority stream of the scene): the next frame's tile
+     * cull then runs while this frame's geometry kernel still runs, instead of after it on the launch stream.
+     * slotUsed[h]: an overlapped launch used slot h (its sky pass ends at evSkyDone[h], its launch-stream kernels at
+     * evGeoDone[h]: a later launch's cull waits for both before rewriting the slot) */
+    hipStream_t cst;
+    bool slotUsed[kSkySlots];
+    hipEvent_t evCullSync; /* the launch stream's position when the culls move to `cst` */
     bool skyPending[kSkySlots];
     SkyKey skyKey[kSkySlots];
-    hipEvent_t evSkyDone[kSkySlots], evGeoDone;
+    hipEvent_t evSkyDone[kSkySlots], evGeoDone[kSkySlots];
     hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
     /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
      * sample order at the kernel's end by the wave that rendered the pixel (grown on demand, <= kSampleBufBudget
@@ -489,10 +500,11 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
     if (e == hipSuccess)
         e = hipMalloc(&s->spheres, ds.size() * sizeof(DevSphere));
+    s->primStride = dt.size();
     if (e == hipSuccess)
-        e = hipMalloc(&s->primF, dt.size() * sizeof(DevPrimF));
+        e = hipMalloc(&s->primF, kSkySlots * dt.size() * sizeof(DevPrimF));
     if (e == hipSuccess)
-        e = hipMalloc(&s->primX, dt.size() * sizeof(DevPrimX));
+        e = hipMalloc(&s->primX, kSkySlots * dt.size() * sizeof(DevPrimX));
     if (e == hipSuccess)
         e = hipMalloc(&s->segSlots, 256 * 16 * sizeof(unsigned long long));
     if (e == hipSuccess) /* kept zero between launches by rtc_reduce_segments */
@@ -512,6 +524,10 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
         e = hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio);
     if (e == hipSuccess) /* the sky tiles yield to the heavy tiles */
         e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, leastPrio);
+    if (e == hipSuccess) /* the next frame's cull goes first wherever a CU frees up */
+        e = hipStreamCreateWithPriority(&s->cst, hipStreamNonBlocking, greatestPrio);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&s->evCullSync, kOrderEventFlags);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&s->evFork, kOrderEventFlags);
     if (e == hipSuccess)
@@ -519,8 +535,9 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     for (int h = 0; h < kSkySlots; ++h)
         if (e == hipSuccess)
             e = hipEventCreateWithFlags(&s->evSkyDone[h], kOrderEventFlags);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evGeoDone, kOrderEventFlags);
+    for (int h = 0; h < kSkySlots; ++h)
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&s->evGeoDone[h], kOrderEventFlags);
     for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
         if (e == hipSuccess)
             e = hipEventCreate(ev);
@@ -541,6 +558,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
     (void)hipSetDevice(s->device);
     if (s->side) /* an unjoined sky pass (RTC_F_OVERLAP) may still read the scratch */
         (void)hipStreamSynchronize(s->side);
+    if (s->cst)
+        (void)hipStreamSynchronize(s->cst);
     if (s->tris)
         (void)hipFree(s->tris);
     if (s->clTris)
@@ -569,14 +588,19 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
         (void)hipEventDestroy(s->evJoin);
-    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evGeoDone})
+    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evCullSync})
         if (ev)
             (void)hipEventDestroy(ev);
     for (hipEvent_t ev : s->evSkyDone)
         if (ev)
             (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : s->evGeoDone)
+        if (ev)
+            (void)hipEventDestroy(ev);
     if (s->side)
         (void)hipStreamDestroy(s->side);
+    if (s->cst)
+        (void)hipStreamDestroy(s->cst);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -2595,6 +2619,9 @@ __host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
 #ifndef RTC_SIDE_STREAM
 #define RTC_SIDE_STREAM 1
 #endif
+#ifndef RTC_CULL_STREAM
+#define RTC_CULL_STREAM 1
+#endif
 #ifdef RTC_AB_NO_SLOTS
 #define RTC_AB_NO_SLOTS_ON 1
 #else
@@ -2673,8 +2700,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.env = env_of(*scene);
     dim3 grid((d->width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
     hipStream_t st = (hipStream_t)stream;
-    P.primF = s->primF;
-    P.primX = s->primX;
+    /* (P.primF / P.primX: the scratch slot's copy, below) */
     /* tile candidate lists (one bit-set per 8x8 tile, 4 per workgroup), workgroup and tile weights and the
      * dispatch order, in one scratch buffer grown on demand (hipFree synchronises, so a previous launch still
      * reading the old buffer has finished) */
@@ -2694,6 +2720,14 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * that counts segments joins, the reduction reads the sky kernel's counters) */
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
     const int half = overlap ? s->flip : 0; /* the scratch slot this launch writes */
+    P.primF = s->primF + (size_t)half * s->primStride;
+    P.primX = s->primX + (size_t)half * s->primStride;
+    /* the stream of the preparation and the culls: for an overlapped small share (the 1080p frame's 1/8, whose
+     * geometry kernel is the critical path) the scene's high-priority cull stream, so the next frame's cull runs
+     * beside this frame's geometry kernel (round 4: 1/8 share 0.089 -> 0.084 ms); a whole frame keeps them on the
+     * launch stream (there the early cull holds CUs the geometry kernel waits for: 0.347 -> 0.361 ms) */
+    const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
+    hipStream_t cs = overlap && smallShare && RTC_CULL_STREAM ? s->cst : st;
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
      * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
@@ -2706,8 +2740,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const SkyKey key = sky_key(P);
     bool mustWait = false;
     for (int h = 0; h < kSkySlots; ++h)
-        if (s->skyPending[h])
-            mustWait = mustWait || !overlap || h == half ||
+        if (s->skyPending[h]) /* (with `cs` the cull stream waits for the pass reading its slot itself, below) */
+            mustWait = mustWait || !overlap || (h == half && cs == st) ||
                        ((s->skyKey[h].colors == key.colors || (key.accum && s->skyKey[h].accum == key.accum)) &&
                         memcmp(&s->skyKey[h], &key, sizeof key) != 0);
     if (mustWait) {
@@ -2756,8 +2790,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                                              (size_t)kGeoLists * geoCap) - s->scratch) + 7) & ~(size_t)7;
         superMask = (unsigned long long *)(s->scratch + off);
     }
-    /* a small share of a row-partitioned frame (the 1080p frame's 1/8): its chain kernel is the critical path */
-    const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
     if (chain) {
         P.geoCount = s->geoCounts + (size_t)(s->geoSeq % kGeoRing) * kGeoSetInts;
         P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
@@ -2790,21 +2822,35 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * zeroed by the previous split launch's tile cull on this stream -- frames of one camera position (round 3:
      * a 5 us kernel at the head of every frame) */
     const float org[3] = {P.origin.x, P.origin.y, P.origin.z};
-    const bool prepCurrent = s->prepValid && s->prepStream == st && memcmp(s->prepOrigin, org, sizeof org) == 0;
-    const bool countsZeroed = !chain || (s->cullValid && s->cullStream == st);
+    if (cs != st) {
+        /* the cull stream rewrites slot `half`: after the earlier launch that used it (its sky pass and its
+         * launch-stream kernels), and after the launch stream's current position when the culls move over from it
+         * (a cull enqueued there may still zero this launch's counter set) */
+        if (s->slotUsed[half]) {
+            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[half], 0));
+            HIP_TRY(hipStreamWaitEvent(cs, s->evGeoDone[half], 0));
+        }
+        if (s->cullStream != cs) {
+            HIP_TRY(hipEventRecord(s->evCullSync, st));
+            HIP_TRY(hipStreamWaitEvent(cs, s->evCullSync, 0));
+        }
+    }
+    const bool prepCurrent =
+        s->prepValid[half] && s->prepStream[half] == cs && memcmp(s->prepOrigin[half], org, sizeof org) == 0;
+    const bool countsZeroed = !chain || (s->cullValid && s->cullStream == cs);
     /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
      * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
     if (chain)
         ms->cullValid = false;
     if ((s->triPadded > 0 || chain) && !(prepCurrent && countsZeroed)) {
-        ms->prepValid = false;
-        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, st, s->tris,
-                           s->primF, s->primX, s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin,
-                           chain ? P.geoCount : nullptr);
+        ms->prepValid[half] = false;
+        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, cs, s->tris,
+                           const_cast<DevPrimF *>(P.primF), const_cast<DevPrimX *>(P.primX),
+                           s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, chain ? P.geoCount : nullptr);
         HIP_TRY(hipGetLastError());
-        ms->prepValid = true;
-        ms->prepStream = st;
-        memcpy(ms->prepOrigin, org, sizeof org);
+        ms->prepValid[half] = true;
+        ms->prepStream[half] = cs;
+        memcpy(ms->prepOrigin[half], org, sizeof org);
     }
     /* level 0 pays for its extra launch on large frames only (1080p: -7 us per frame); a small share (the 1/8 of a
      * row-partitioned 1080p frame) culls faster without it (round 4 A/B: 0.111 vs 0.118 ms per joined share) */
@@ -2812,18 +2858,20 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     if (cull && superMask && superCull && s->maskWords > 0) {
         P.superMask = superMask;
         P.superX = (int)superGrid.x;
-        hipLaunchKernelGGL(rtc_super_cull, superGrid, dim3(64), 0, st, P, superMask);
+        hipLaunchKernelGGL(rtc_super_cull, superGrid, dim3(64), 0, cs, P, superMask);
         HIP_TRY(hipGetLastError());
     }
     if (cull) {
         /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
-        HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), st,
+        HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), cs,
                             fused && RTC_SIDE_STREAM ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
-        if (chain) { /* this cull zeroes the next set's counters (P.geoCountNext) on `st` */
+        if (chain) { /* this cull zeroes the next set's counters (P.geoCountNext) on `cs` */
             ms->geoSeq++;
             ms->cullValid = true;
-            ms->cullStream = st;
+            ms->cullStream = cs;
         }
+        if (cs != st) /* the geometry kernel after the cull */
+            HIP_TRY(hipStreamWaitEvent(st, s->evFork, 0));
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (fused) {
@@ -2864,7 +2912,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                                                 floorLds > kChainStaticLds ? floorLds - kChainStaticLds : 0);
             /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
-            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone : nullptr;
+            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone[half] : nullptr;
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, st, chainStop, P));
@@ -2878,7 +2926,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evHeavy1, st));
             if (P.sampleCap > 0 && !RTC_AB_NO_SLOTS_ON) {
                 const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, overlap ? s->evGeoDone : nullptr, P));
+                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, overlap ? s->evGeoDone[half] : nullptr,
+                                    P));
                 HIP_TRY(hipGetLastError());
             }
             if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
@@ -2889,9 +2938,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (overlap) {
                 /* no join: the frame is complete once the side stream has passed both passes (evGeoDone: recorded
                  * by the last kernel above) */
-                HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone, 0));
+                HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone[half], 0));
                 if (frameEvent)
                     HIP_TRY(hipEventRecord(frameEvent, s->side));
+                ms->slotUsed[half] = true;
                 ms->flip = (ms->flip + 1) % kSkySlots;
                 return 0;
             }
