@@ -164,6 +164,9 @@ __device__ __forceinline__ float random_normal(unsigned &s)
     float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)random_value(s)));
     return (float)((double)rho * rtcmath::cos((double)theta));
 }
+#ifndef RTC_BM_FALLBACK_SERIAL
+#define RTC_BM_FALLBACK_SERIAL 0
+#endif
 /* the exact restatement of three normals (the fallback of random_direction); inlined (out of line, with
  * RTC_BM_NOINLINE_FALLBACK, the chain kernel spills less but runs ~1.5% slower) */
 #ifdef RTC_BM_NOINLINE_FALLBACK
@@ -171,9 +174,23 @@ __attribute__((noinline))
 #endif
 static __device__ __forceinline__ void random_normals_exact(unsigned &s, float v[3])
 {
+#if RTC_BM_FALLBACK_SERIAL
+    /* one normal at a time (a loop that is not unrolled): the rare fallback's live registers are one normal's, not
+     * three interleaved normals' -- they set the chain kernel's peak register pressure */
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+        const float n = random_normal(s);
+        a = k == 0 ? n : a;
+        b = k == 1 ? n : b;
+        c = k == 2 ? n : c;
+    }
+    v[0] = a, v[1] = b, v[2] = c;
+#else
     v[0] = random_normal(s);
     v[1] = random_normal(s);
     v[2] = random_normal(s);
+#endif
 }
 /* RandomDiretion (moremath.c:104-108), components drawn x, y, z.  The three normals take the certified fast
  * path (rtc_math.h bm_rho_fast / bm_normal_fast: table-driven log and cos, each float returned only when it
@@ -202,10 +219,15 @@ __device__ __forceinline__ V3 random_direction(unsigned &s, const rtcmath::BmLog
         ok = rtcmath::bm_rho_fast(random_value(s), rho, logTab) && ok;
         ok = rtcmath::bm_normal_fast(rho, theta, v[c], cosTab) && ok;
     }
+#ifndef RTC_AB_NO_BM_FALLBACK /* timing experiment only (the exact fallback's register cost): not the reference */
     if (__builtin_expect(!ok, 0)) {
         s = s0;
         random_normals_exact(s, v);
     }
+#else
+    (void)ok;
+    (void)s0;
+#endif
     return normalized(V3{v[0], v[1], v[2]});
 #else
     float a = random_normal(s);
