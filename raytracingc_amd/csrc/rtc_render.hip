@@ -1909,6 +1909,16 @@ constexpr int kChainBlock = 256;
  * Compared with a wave-uniform loop over the union of the lanes' clusters (every lane masked through every
  * cluster some lane needs), each ray-triangle test here occupies one lane-slot instead of up to 64. */
 typedef float f2 __attribute__((ext_vector_type(2)));
+/* A sample's m-th hit draws the 7 values at state index j + m (RandomDiretion's six, the roulette's one): exactly
+ * what S_{j+m}'s first hit draws.  So the window's active lanes enter the draws of their own state index, computed
+ * at the primary hit, in a per-wave LDS table, and a later hit of lane l in bounce iteration i reads entry l + i
+ * instead of running Box-Muller again; only lanes with l + i past the window's active lanes compute theirs (the
+ * state advanced by 7 i draws).  The values are the same function of the same state, so the frame is unchanged;
+ * what goes is most of the divergent Box-Muller passes of the bounce iterations with a hit (scenes whose rays hit
+ * several times: fsuzane 2.00 -> 1.93 ms per frame, 1.77 with the dense culls below). */
+#ifndef RTC_DRAW_TABLE
+#define RTC_DRAW_TABLE 1
+#endif
 #ifndef RTC_CHAIN_PAIRS
 #define RTC_CHAIN_PAIRS 1024
 #endif
@@ -1919,13 +1929,17 @@ struct ChainWaveLds {
      * refilled.  Its size keeps a block (4 waves + the staged records of one chunk) within 40 KB of LDS: four
      * blocks per CU, the 4 waves per SIMD that 128 VGPRs allow */
     unsigned short pair[RTC_CHAIN_PAIRS];
+#if RTC_DRAW_TABLE
+    float4 draw[64]; /* the window's hit draws by state index jn + i: RandomDirection's vector, the roulette value */
+#endif
 };
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
 static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
-constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64;
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
+                                   kChunkClusters * sizeof(DevCluster) /* sCl (RTC_DENSE_CULL) */;
 constexpr size_t kCuLds = 160 * 1024; /* gfx950 LDS per CU */
 /* the block LDS that keeps the chain workgroups per CU at most n: above kCuLds / (n + 1) */
 constexpr size_t chain_lds_floor(int n) { return n >= 4 ? 0 : kCuLds / (size_t)(n + 1) + 256; }
@@ -2010,10 +2024,24 @@ __device__ __forceinline__ void chain_pair_passes_cl(int n, const float4 *__rest
     }
 }
 
-template <bool MULTI>
+/* Dense cluster culls (single-chunk scenes, bounce segments after the first): with a live lanes and nCl clusters, the
+ * per-lane loop issues nCl culls for the wave however few lanes are live; instead the wave takes the a * nCl (live
+ * lane, cluster) culls 64 at a time -- cluster-major, so the pairs kept come out in the per-lane loop's order -- the
+ * owner's ray by ds_bpermute, the cluster from LDS.  Taken while a <= RTC_DENSE_CULL_MAX (fsuzane 1.93 -> 1.77 ms per
+ * frame with 16, 1.80 with 32; the headline frame, whose later bounces are rare, within noise). */
+#ifndef RTC_DENSE_CULL
+#define RTC_DENSE_CULL 1
+#endif
+#ifndef RTC_DENSE_CULL_MAX
+#define RTC_DENSE_CULL_MAX 16
+#endif
+static_assert(RTC_DENSE_CULL_MAX * kChunkClusters <= RTC_CHAIN_PAIRS, "a dense cull's pairs fit the list");
+static_assert(sizeof(ChainWaveLds::cl) >= 64 * sizeof(int), "the dense cull's owner lanes fit W.cl");
+
+template <bool MULTI, bool COUNT>
 __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, bool firstBounce, V3 pos,
                                                      V3 dir, const float4 *__restrict__ sRec, ChainWaveLds &W,
-                                                     int lane, unsigned &tests)
+                                                     int lane, unsigned &tests, const DevCluster *__restrict__ sCl)
 {
     W.key[lane] = kNoHitKey;
     const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z), dd = dir_dd(dir);
@@ -2081,10 +2109,57 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                 continue;
         }
         unsigned cm = 0;
+        int n = 0;
         DSECT_BEGIN(dc3);
+#if RTC_DENSE_CULL
+        const unsigned long long inM = __ballot(in);
+        const int nIn = (int)__popcll(inM);
+        const bool dense = !MULTI && !table && nIn <= RTC_DENSE_CULL_MAX;
+        if (dense) {
+            int *own = (int *)&W.cl[0][0]; /* W.cl is free outside the first bounce's table mode */
+            int *kept = own + 64;          /* COUNT: per owner lane, clusters kept (+ 1 << 16 for the scene's last) */
+            if (in)
+                own[__builtin_amdgcn_mbcnt_hi((unsigned)(inM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)inM, 0u))] = lane;
+            if (COUNT)
+                kept[lane] = 0;
+            wave_lds_sync();
+            const int tot = nIn * nCl;
+            const unsigned magic = nIn > 1 ? (unsigned)((0x100000000ull + (unsigned)nIn - 1u) / (unsigned)nIn) : 0u;
+            for (int b = 0; b < tot; b += 64) {
+                const int e = b + lane;
+                const int k = nIn > 1 ? (int)__umulhi((unsigned)e, magic) : e; /* e / nIn, exact for e < 2^16 */
+                const bool valid = e < tot;
+                const int o = own[valid ? e - k * nIn : 0];
+                const V3 rp{bperm_f(o, pos.x), bperm_f(o, pos.y), bperm_f(o, pos.z)};
+                const V3 rd{bperm_f(o, dir.x), bperm_f(o, dir.y), bperm_f(o, dir.z)};
+                bool keep = false;
+                if (valid) {
+                    const float rr = fabsf(rd.x) + fabsf(rd.y) + fabsf(rd.z);
+                    keep = !(P.clusterCull && rr <= kClusterRhoMax && cluster_culled(rp, rd, rr, dir_dd(rd), sCl[k]));
+                }
+                const unsigned long long m = __ballot(keep);
+                if (keep)
+                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                        (unsigned short)(o | (k << 6));
+                if (COUNT && keep)
+                    atomicAdd(&kept[o], 1 + (k == P.clusterCount - 1 ? 1 << 16 : 0));
+                n += (int)__popcll(m);
+            }
+            if (COUNT) {
+                wave_lds_sync();
+                const int kc = kept[lane];
+                tests = (unsigned)(kc & 0xffff) * kClusterSize -
+                        (unsigned)(kc >> 16) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+            }
+        }
+#else
+        constexpr bool dense = false;
+#endif
         /* table mode: bit j of cm = the j-th live cluster kept (branch-free body over the compacted terms) */
         const int nLive = __popcll(live);
-        if (in && table) {
+        if (dense) {
+        } else if (in && table) {
 #pragma unroll 4
             for (int j = 0; j < nLive; ++j) {
                 const float4 a = W.cl[j][0], b = W.cl[j][1];
@@ -2103,9 +2178,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         }
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
-        int n = 0;
         constexpr int kCap = RTC_CHAIN_PAIRS;
-        if (table) {
+        if (dense) {
+        } else if (table) {
             /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
              * whenever the next cluster would overflow it */
             for (int j = 0; j < nLive; ++j) {
@@ -2266,6 +2341,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
+#if RTC_DENSE_CULL
+    __shared__ DevCluster sCl[kChunkClusters]; /* single-chunk scenes: the clusters, for the dense culls */
+    if (!MULTI && threadIdx.x < P.clusterCount && threadIdx.x < kChunkClusters)
+        sCl[threadIdx.x] = P.clusters[threadIdx.x];
+#else
+    const DevCluster *sCl = nullptr;
+#endif
     if (threadIdx.x == 0)
         sWork = 0;
     sPow.fill(threadIdx.x);
@@ -2384,12 +2466,18 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     DSECT_END(dc1, 1);
                 } else { /* bounce segments of the live lanes (the whole wave takes part) */
                     unsigned t = 0;
-                    c = chain_trace_pairs<MULTI>(P, alive, bounce1, pos, dir, sRec, W, lane, t);
+                    c = chain_trace_pairs<MULTI, COUNT>(P, alive, bounce1, pos, dir, sRec, W, lane, t, sCl);
                     if (counting && alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
                     }
                 }
+#if RTC_DRAW_TABLE
+                /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
+                RngJump J{1u, 0u};
+                if (!first && __ballot(alive && c.idx >= 0 && lane + iter >= nAct))
+                    J = rng_jump_by(7u * (unsigned)iter); /* wave-uniform */
+#endif
                 if (alive) {
                     if (counting)
                         calls++;
@@ -2410,7 +2498,24 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             M = P.mats[c.idx];
                         }
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
+#if RTC_DRAW_TABLE
+                        /* the hit draws (see RTC_DRAW_TABLE): the primary hit computes the lane's own and enters
+                         * them in the table (every active lane hits there: one primary ray per wave); a later hit
+                         * reads entry lane + iter, or computes it when that is past the window's active lanes */
+                        float4 D;
+                        if (first || lane + iter >= nAct) {
+                            unsigned s = first ? rng : rng * J.a + J.c;
+                            const V3 rd = random_direction(s);
+                            D = make_float4(rd.x, rd.y, rd.z, random_value(s));
+                            if (first)
+                                W.draw[lane] = D; /* read in later iterations, after chain_trace_pairs' LDS syncs */
+                        } else {
+                            D = W.draw[lane + iter];
+                        }
+                        const V3 diffuseDir = normalized(add(normal, V3{D.x, D.y, D.z}));
+#else
                         const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+#endif
                         const V3 specularDir = reflect(dir, normal);
                         dir = lerp(diffuseDir, specularDir, M.smoothness);
                         pos = hitPoint;
@@ -2418,7 +2523,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         light = add(light, mulv(emitted, rayColor));
                         rayColor = mulv(rayColor, color);
                         const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
+#if RTC_DRAW_TABLE
+                        endSample = p < D.w;
+#else
                         endSample = p < random_value(rng);
+#endif
                         if (!endSample) {
                             rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
                             bounce++;
