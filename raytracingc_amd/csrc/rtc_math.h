@@ -332,6 +332,25 @@ RTC_HD float powf_exp2(double xd, unsigned signBias,
     return (float)y;
 }
 
+/* powf(x, y) for a special y (+-0, +-inf, NaN: powf_zeroinfnan(iy)), any x -- e_powf.c's first special case */
+RTC_HD float powf_special_y(float x, float y)
+{
+    const unsigned ix = f2u(x), iy = f2u(y);
+    /* signalling NaN: quiet bit clear */
+    auto sig = [](unsigned u) { return (u & 0x7fc00000u) == 0x7f800000u && (u & 0x003fffffu) != 0; };
+    if (2 * iy == 0)
+        return sig(ix) ? x + y : 1.0f;
+    if (ix == 0x3f800000u)
+        return sig(iy) ? x + y : 1.0f;
+    if (2 * ix > 2u * 0x7f800000u || 2 * iy > 2u * 0x7f800000u)
+        return x + y;
+    if (2 * ix == 2u * 0x3f800000u)
+        return 1.0f;
+    if ((2 * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u))
+        return 0.0f;
+    return y * y;
+}
+
 template <bool FMA>
 RTC_HD float powf_glibc(float x, float y, const double (*log2tab)[2] = powf_data::kLog2Tab,
                         const unsigned long long *exp2tab = powf_data::kExp2Tab) /* e_powf.c __powf, round-to-nearest */
@@ -339,21 +358,8 @@ RTC_HD float powf_glibc(float x, float y, const double (*log2tab)[2] = powf_data
     unsigned signBias = 0;
     unsigned ix = f2u(x), iy = f2u(y);
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || powf_zeroinfnan(iy)) {
-        if (powf_zeroinfnan(iy)) {
-            /* signalling NaN: quiet bit clear */
-            auto sig = [](unsigned u) { return (u & 0x7fc00000u) == 0x7f800000u && (u & 0x003fffffu) != 0; };
-            if (2 * iy == 0)
-                return sig(ix) ? x + y : 1.0f;
-            if (ix == 0x3f800000u)
-                return sig(iy) ? x + y : 1.0f;
-            if (2 * ix > 2u * 0x7f800000u || 2 * iy > 2u * 0x7f800000u)
-                return x + y;
-            if (2 * ix == 2u * 0x3f800000u)
-                return 1.0f;
-            if ((2 * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u))
-                return 0.0f;
-            return y * y;
-        }
+        if (powf_zeroinfnan(iy))
+            return powf_special_y(x, y);
         if (powf_zeroinfnan(ix)) {
             float x2 = x * x;
             if ((ix & 0x80000000u) && powf_checkint(iy) == 1)
