@@ -244,7 +244,8 @@ struct EnvParams {
     V3 sun, horizon, zenith, ground;
     float focus, intensity;
     bool sunSkip; /* env_sun_skippable(focus, intensity) */
-    /* powf tables (null: glibc's constants in global memory; kernels point them at LDS copies) */
+    /* powf tables: every kernel that evaluates the environment points them at its LDS copies (PowTablesLds; round 4:
+     * no null-table branch to glibc's constants in global memory, whose code the sky kernel paid for in spills) */
     const double (*log2tab)[2];
     const unsigned long long *exp2tab;
 };
@@ -260,8 +261,7 @@ __device__ __forceinline__ float pow_ref(float x, float y, const EnvParams &s)
     const unsigned iy = rtcmath::f2u(y);
     if (!rtcmath::powf_zeroinfnan(iy)) {
         const float ax = __builtin_fabsf(x);
-        const float r =
-            s.log2tab ? rtcmath::powf_glibc_pos<true>(ax, y, s.log2tab, s.exp2tab) : rtcmath::powf_glibc_pos<true>(ax, y);
+        const float r = rtcmath::powf_glibc_pos<true>(ax, y, s.log2tab, s.exp2tab);
         const bool odd = rtcmath::powf_checkint(iy) == 1; /* uniform */
         return (odd && rtcmath::f2u(x) == 0x80000000u) ? -r : r;
     }
@@ -317,10 +317,9 @@ __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s)
 #define RTC_SKY_UNIT 1
 #endif
     if (RTC_SKY_UNIT && __all(sa - 0x00800000u <= 0x3f800000u - 0x00800000u)) /* every lane normal x in (0, 1]: main path */
-        skyGradientT = s.log2tab ? rtcmath::powf_sky_unit(skyArg, s.log2tab, s.exp2tab) : rtcmath::powf_sky_unit(skyArg);
+        skyGradientT = rtcmath::powf_sky_unit(skyArg, s.log2tab, s.exp2tab);
     else if (__any(sa != 0u))
-        skyGradientT = s.log2tab ? rtcmath::powf_glibc_pos<true>(skyArg, 0.35f, s.log2tab, s.exp2tab)
-                                 : rtcmath::powf_glibc_pos<true>(skyArg, 0.35f);
+        skyGradientT = rtcmath::powf_glibc_pos<true>(skyArg, 0.35f, s.log2tab, s.exp2tab);
     V3 skyGradient = lerp(s.horizon, s.zenith, skyGradientT);
     const float sunArg = fmax0_ref(dot(dir, s.sun));
     float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);

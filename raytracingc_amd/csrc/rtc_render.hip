@@ -3179,11 +3179,15 @@ __global__ void probe_sphere_kernel(const Ray *rays, const Sphere *sph, size_t n
 
 __global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n, vec3 *out)
 {
+    __shared__ PowTablesLds sPow; /* the environment reads its powf tables from LDS, as in the render kernels */
+    sPow.fill(threadIdx.x);
+    __syncthreads();
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     Scene s = scenes[i];
     EnvParams e{};
+    sPow.attach(e);
     e.sun = v3(s.normalizedSunDirection);
     e.horizon = v3(s.skyColorHorizon);
     e.zenith = v3(s.skyColorZenith);
