@@ -206,6 +206,7 @@ struct RtcDeviceScene {
      * slotUsed[h]: an overlapped launch used slot h (its sky pass ends at evSkyDone[h], its launch-stream kernels at
      * evGeoDone[h]: a later launch's cull waits for both before rewriting the slot) */
     hipStream_t cst;
+    hipStream_t cst2; /* RTC_SHARE_CHAIN_CS: the second cull stream (odd slots) */
     bool slotUsed[kSkySlots];
     hipEvent_t evCullSync; /* the launch stream's position when the culls move to `cst` */
     bool skyPending[kSkySlots];
@@ -560,6 +561,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipStreamSynchronize(s->side);
     if (s->cst)
         (void)hipStreamSynchronize(s->cst);
+    if (s->cst2)
+        (void)hipStreamSynchronize(s->cst2);
     if (s->tris)
         (void)hipFree(s->tris);
     if (s->clTris)
@@ -601,6 +604,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipStreamDestroy(s->side);
     if (s->cst)
         (void)hipStreamDestroy(s->cst);
+    if (s->cst2)
+        (void)hipStreamDestroy(s->cst2);
     if (cur >= 0)
         (void)hipSetDevice(cur);
     delete s;
@@ -1876,8 +1881,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_
  * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
  * Work: one wave per geometry pixel, from the tile cull's sub-lists (see the kernel). */
+#ifndef RTC_SHARE_CHAIN_CS
+#define RTC_SHARE_CHAIN_CS 1
+#endif
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
-constexpr size_t kInlineSumPixels = 400000;          /* shares (row stride > 1) up to this many pixels sum in-kernel */
+/* Shares (row stride > 1) of up to this many pixels are "small": they sum in-kernel, run 4 chain workgroups per CU and,
+ * pipelined, prepare, cull and run their geometry kernel on the two cull streams (RTC_SHARE_CHAIN_CS).  Round 4 raised it
+ * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
+ * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
+#ifndef RTC_INLINE_SUM_PIXELS
+#define RTC_INLINE_SUM_PIXELS 600000
+#endif
+constexpr size_t kInlineSumPixels = RTC_INLINE_SUM_PIXELS;
 constexpr int kChainBlock = 256;
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
@@ -2836,7 +2851,21 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * beside this frame's geometry kernel (round 4: 1/8 share 0.089 -> 0.084 ms); a whole frame keeps them on the
      * launch stream (there the early cull holds CUs the geometry kernel waits for: 0.347 -> 0.361 ms) */
     const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
-    hipStream_t cs = overlap && smallShare && RTC_CULL_STREAM ? s->cst : st;
+    /* RTC_SHARE_CHAIN_CS: an overlapped small share prepares, culls AND runs its geometry kernel on one of two cull
+     * streams, by slot parity: no cross-stream wait between its cull and its geometry kernel (round 4: ~12 us per share
+     * frame), its cull still runs beside the previous launch's geometry kernel (on the other stream), and its geometry
+     * kernel is not ordered after that one, whose tail it fills (they share nothing: other scratch slot, counter set and
+     * Color buffer; small shares sum in-kernel).  The previous launch's cull (which zeroes this launch's counter set)
+     * is ordered before this one's by its event; `st` waits for the geometry kernel at the end of the launch. */
+    const bool chainOnCs = RTC_SHARE_CHAIN_CS && overlap && smallShare && RTC_CULL_STREAM;
+    if (chainOnCs && !s->cst2) { /* created on first use: whole frames keep three streams (one more costs them ~1 %) */
+        int leastPrio = 0, greatestPrio = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
+        HIP_TRY(hipStreamCreateWithPriority(&ms->cst2, hipStreamNonBlocking, greatestPrio));
+    }
+    hipStream_t cs = chainOnCs ? ((half & 1) ? s->cst2 : s->cst) : overlap && smallShare && RTC_CULL_STREAM ? s->cst : st;
+    hipStream_t gs = chainOnCs ? cs : st; /* the geometry kernel's stream */
+    const bool altStreams = chainOnCs && (s->cullStream == s->cst || s->cullStream == s->cst2);
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
      * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
@@ -2855,6 +2884,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                         memcmp(&s->skyKey[h], &key, sizeof key) != 0);
     if (mustWait) {
         HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[s->lastSky], 0));
+        if (chainOnCs) /* the geometry kernel writes Color rows on `cs` */
+            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[s->lastSky], 0));
         for (int h = 0; h < kSkySlots; ++h)
             ms->skyPending[h] = false;
     }
@@ -2939,14 +2970,17 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[half], 0));
             HIP_TRY(hipStreamWaitEvent(cs, s->evGeoDone[half], 0));
         }
-        if (s->cullStream != cs) {
+        if (altStreams) {
+            /* the previous launch's cull (the other cull stream) zeroes this launch's counter set */
+            HIP_TRY(hipStreamWaitEvent(cs, s->evFork, 0));
+        } else if (s->cullStream != cs) {
             HIP_TRY(hipEventRecord(s->evCullSync, st));
             HIP_TRY(hipStreamWaitEvent(cs, s->evCullSync, 0));
         }
     }
     const bool prepCurrent =
         s->prepValid[half] && s->prepStream[half] == cs && memcmp(s->prepOrigin[half], org, sizeof org) == 0;
-    const bool countsZeroed = !chain || (s->cullValid && s->cullStream == cs);
+    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || altStreams));
     /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
      * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
     if (chain)
@@ -2979,7 +3013,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             ms->cullValid = true;
             ms->cullStream = cs;
         }
-        if (cs != st) /* the geometry kernel after the cull */
+        if (cs != st && !chainOnCs) /* the geometry kernel after the cull */
             HIP_TRY(hipStreamWaitEvent(st, s->evFork, 0));
         P.tileMask = mask;
         P.pixMask = pixMask;
@@ -3009,7 +3043,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 ms->lastSky = half;
             }
             if (s->timing)
-                HIP_TRY(hipEventRecord(s->evHeavy0, st));
+                HIP_TRY(hipEventRecord(s->evHeavy0, gs));
             /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
              * filter records when the block stays within 4 per CU */
             const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : RTC_CHAIN_WGS_FULL;
@@ -3024,23 +3058,23 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone[half] : nullptr;
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, st, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, gs, chainStop, P));
             else if (s->chunkCount > 1)
-                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, dyn, st, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, dyn, gs, chainStop, P));
             else if (dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, dyn, st, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, dyn, gs, chainStop, P));
             else
-                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, st, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, gs, chainStop, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
-                HIP_TRY(hipEventRecord(s->evHeavy1, st));
+                HIP_TRY(hipEventRecord(s->evHeavy1, gs));
             if (P.sampleCap > 0 && !RTC_AB_NO_SLOTS_ON) {
                 const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, st, overlap ? s->evGeoDone[half] : nullptr,
+                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, gs, overlap ? s->evGeoDone[half] : nullptr,
                                     P));
                 HIP_TRY(hipGetLastError());
             }
             if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
-                HIP_TRY(hipEventRecord(geoEvent, st));
+                HIP_TRY(hipEventRecord(geoEvent, gs));
                 geoRecorded = true;
             }
             ms->timed = s->timing;
@@ -3048,6 +3082,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 /* no join: the frame is complete once the side stream has passed both passes (evGeoDone: recorded
                  * by the last kernel above) */
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone[half], 0));
+                if (chainOnCs) /* the launch stream holds the geometry pass too */
+                    HIP_TRY(hipStreamWaitEvent(st, s->evGeoDone[half], 0));
                 if (frameEvent)
                     HIP_TRY(hipEventRecord(frameEvent, s->side));
                 ms->slotUsed[half] = true;
