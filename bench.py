@@ -350,13 +350,15 @@ def main():
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < 0.3:
         loop(cfg_r, 10)
-    # per-kernel device times of the split launch (HIP events the library records around rtc_render_chain on the
-    # launch stream and around rtc_render_sky on the scene's side stream), averaged over joined frames rendered back
-    # to back at settled clocks, like rocprofv3's kernel trace of the same command
+    # per-kernel device times of the split launch (HIP events the library records around rtc_render_chain on its
+    # stream and around rtc_render_sky on the scene's side stream), averaged over frames launched like the timed ones
+    # (RTC_F_OVERLAP: in-kernel sums, the cull streams), one at a time at settled clocks, like rocprofv3's kernel trace
+    # of the same command
     kt = []
+    cfg_t = dataclasses_replace(cfg_r, overlap=True)
     ds.set_timing(True)
     for _ in range(20):
-        ds.render_rows_async(scene, cam, cfg_r, dev_rows[0].data_ptr(), None, None, stream.cuda_stream)
+        ds.render_rows_async(scene, cam, cfg_t, dev_rows[0].data_ptr(), None, None, stream.cuda_stream)
         k = ds.kernel_times()
         if k:
             kt.append(k)

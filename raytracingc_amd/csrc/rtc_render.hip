@@ -2851,13 +2851,18 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * beside this frame's geometry kernel (round 4: 1/8 share 0.089 -> 0.084 ms); a whole frame keeps them on the
      * launch stream (there the early cull holds CUs the geometry kernel waits for: 0.347 -> 0.361 ms) */
     const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
-    /* RTC_SHARE_CHAIN_CS: an overlapped small share prepares, culls AND runs its geometry kernel on one of two cull
-     * streams, by slot parity: no cross-stream wait between its cull and its geometry kernel (round 4: ~12 us per share
-     * frame), its cull still runs beside the previous launch's geometry kernel (on the other stream), and its geometry
-     * kernel is not ordered after that one, whose tail it fills (they share nothing: other scratch slot, counter set and
-     * Color buffer; small shares sum in-kernel).  The previous launch's cull (which zeroes this launch's counter set)
-     * is ordered before this one's by its event; `st` waits for the geometry kernel at the end of the launch. */
-    const bool chainOnCs = RTC_SHARE_CHAIN_CS && overlap && smallShare && RTC_CULL_STREAM;
+    /* RTC_SHARE_CHAIN_CS: an overlapped launch prepares, culls AND runs its geometry kernel on one of two cull streams,
+     * by slot parity: no cross-stream wait between its cull and its geometry kernel (round 4: ~12 us per 1080p 1/8 share
+     * frame), its cull runs beside the previous launch's geometry kernel (on the other stream), and its geometry kernel
+     * is not ordered after that one, whose tail it fills.  They share nothing: other scratch slot, counter set and Color
+     * buffer, and these launches sum in-kernel (no sample slots, whole frames included).  The previous launch's cull
+     * (which zeroes this launch's counter set) is ordered before this one's by its event; `st` waits for the geometry
+     * kernel at the end of the launch.  Round 4: 1/8 share 0.087 -> 0.079 ms, whole frame 0.343 -> 0.339 ms
+     * (RTC_ALT_FULL; its tile cull then runs beside the previous frame's kernels, 20 -> ~100 us, off the critical path). */
+#ifndef RTC_ALT_FULL
+#define RTC_ALT_FULL 1 /* whole pipelined frames on the alternating cull streams too */
+#endif
+    const bool chainOnCs = RTC_SHARE_CHAIN_CS && overlap && (smallShare || RTC_ALT_FULL) && RTC_CULL_STREAM;
     if (chainOnCs && !s->cst2) { /* created on first use: whole frames keep three streams (one more costs them ~1 %) */
         int leastPrio = 0, greatestPrio = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
@@ -2940,7 +2945,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
          * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
          * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
          * 4K 1/8 share are faster deferred) */
-        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !RTC_INLINE_ALL) {
+        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !RTC_INLINE_ALL && !chainOnCs) {
             const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
