@@ -1897,13 +1897,15 @@ constexpr int kChainBlock = 256;
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
  * in the chain kernel's idle issue slots instead of waiting for its tail, and the launch stream's small kernels are no
- * longer starved by that tail (round 4: frame 0.372 -> 0.351 ms).  A small share of a row-partitioned frame runs 4 (its
- * chain kernel is the critical path).  Workers = per-CU count x CUs: exactly the resident capacity, no second round. */
+ * longer starved by that tail (round 4: frame 0.372 -> 0.351 ms; 4 per CU: 0.370 vs 0.340 ms on the alternating streams,
+ * though fsuzane, whose frame is nearly all geometry kernel, takes 1.12 vs 1.22 ms with 4).  Small shares run 3 too since
+ * consecutive shares overlap on the alternating streams (4 before).  Workers = per-CU count x CUs: exactly the resident
+ * capacity, no second round. */
 #ifndef RTC_CHAIN_WGS_FULL
 #define RTC_CHAIN_WGS_FULL 3
 #endif
 #ifndef RTC_CHAIN_WGS_SHARE
-#define RTC_CHAIN_WGS_SHARE 4
+#define RTC_CHAIN_WGS_SHARE 3 /* 1/4 share 0.116 -> 0.113 ms, 1/8 share 0.075 -> 0.074 ms (round 4, r04_za) */
 #endif
 #ifndef RTC_CHAIN_UNROLL
 #define RTC_CHAIN_UNROLL 2
