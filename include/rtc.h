@@ -76,7 +76,8 @@ typedef struct RtcRenderDesc {
 #define RTC_F_SPEC          0x100 /* removed: RTC_EINVAL */
 #define RTC_F_CHAIN_INLINE  0x400 /* rtc_render_chain adds each pixel's samples itself instead of deferring the
                                      in-order sum to a separate pass (identical frame; the default for a small share
-                                     of a row-partitioned frame: rowStride > 1 and width * rows <= 400,000) */
+                                     of a row-partitioned frame, rowStride > 1 and width * rows <= 600,000, and for
+                                     the overlapped launches on the alternating streams, RTC_F_OVERLAP) */
 #define RTC_F_HOST_ROWS     0x1000 /* rtc_render_multi only: no gather -- every device copies its rows straight into
                                       their places of the host frame (rtc_copy_rows_d2h_dma, its own PCIe link);
                                       without it the parts are gathered to device 0 over RCCL, re-interleaved there
@@ -87,7 +88,11 @@ typedef struct RtcRenderDesc {
                                      launch waits for it only when it would rewrite its scratch slot (8 launches
                                      later) or writes the same Color / accumulator buffer with other rows, camera or
                                      environment; a later launch that is not overlapped waits for it before its
-                                     first kernel.  The
+                                     first kernel.  Every overlapped launch but a row-stride-1 frame of at most
+                                     600 k pixels prepares, culls and runs its geometry kernel on one of two scene
+                                     streams (alternating), unordered against the previous launch's geometry
+                                     kernel, and sums each pixel's samples in-kernel; `stream` waits for that kernel at the
+                                     launch's end, not for the sky pass.  The
                                      frame is complete when the scene's frame event (rtc_scene_set_frame_event)
                                      fires; with segment counters requested the launch joins as usual.  Same
                                      frame bit for bit. */
