@@ -1775,31 +1775,45 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile of a 16x16 block; the waves of
+/* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile (one-wave workgroups, or four per 16x16 block); the waves of
  * tiles whose pixels all have primary candidates return at once (rtc_render_chain renders those).  Few registers, so many
  * waves per SIMD hide the latency of the environment's double-precision chains. */
 #ifndef RTC_SKY_WAVES
 #define RTC_SKY_WAVES 8 /* <= 64 VGPRs: two sky workgroups fit where one chain workgroup retires (frame -1.5 %, round 4) */
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky(
+/* kSkyWaves waves per workgroup: 4 (a 16x16 block) or 1 (one 8x8 tile).  One-wave workgroups fit the registers and wave
+ * slots the co-resident chain workgroups leave free at a finer grain (round 4: whole 1080p frame -1 %, 4K -0.6 %, the
+ * 1080p 1/8 share -2 %), but the 1/4 share (518 k px) took 3.5 % longer with them, so small shares of more than 400 k
+ * pixels keep 4 (profiles/r04_zd_ab_sky_wg.log) */
+template <int kSkyWaves>
+__global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky(
     RenderParams P, const unsigned *__restrict__ tileW)
 {
+    static_assert(kSkyWaves == 4 || kSkyWaves == 1, "a sky workgroup is a 16x16 block or one 8x8 tile");
     __shared__ PowTablesLds sPow;
-    __shared__ __attribute__((aligned(4))) unsigned char sSkyRow[kBlock / 64][8][24];
+    __shared__ __attribute__((aligned(4))) unsigned char sSkyRow[kSkyWaves][8][24];
     sPow.fill(threadIdx.x);
     __syncthreads();
     sPow.attach(P.env);
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;
     unsigned segCalls = 0, segTraced = 0;
     {
-        const int bx = blockIdx.x, by = blockIdx.y;
+        /* the 16x16 block (bx, by) and this wave's 8x8 tile w16 in it (one-wave workgroups: grid twice as wide and tall) */
+        const int bx = kSkyWaves == 4 ? (int)blockIdx.x : (int)blockIdx.x >> 1;
+        const int by = kSkyWaves == 4 ? (int)blockIdx.y : (int)blockIdx.y >> 1;
+        const int w16 = kSkyWaves == 4 ? __builtin_amdgcn_readfirstlane(lw) : (int)((blockIdx.y & 1) * 2 + (blockIdx.x & 1));
         /* pixels without a primary candidate: their primary ray misses every triangle (the filter is exact-safe),
          * so every sample is one segment ending in the sky, in tiles with geometry pixels too (rtc_render_chain takes only the geometry pixels) */
-        const int t = wave_tile(bx, by);
+        const int t = (by * 2 + (w16 >> 1)) * (P.blocksX * 2) + bx * 2 + (w16 & 1);
         const unsigned long long geo = tileW[t] > 0 ? P.pixMask[t] : 0ull;
         if (geo == ~0ull)
             return;
-        PixelRay px = pixel_ray(P, bx, by);
+        PixelRay px;
+        px.x = bx * kTileW + (w16 & 1) * 8 + (lane & 7);
+        px.r = by * kTileH + (w16 >> 1) * 8 + (lane >> 3);
+        px.valid = px.x < P.width && px.r < P.rows;
+        px.y = P.rowStart + px.r * P.rowStride;
+        px.dir = primary_dir(P, px.x, px.y);
         px.valid = px.valid && !((geo >> lane) & 1ull);
         V3 acc{0.f, 0.f, 0.f};
         if (px.valid && P.spp > 0 && P.maxBounce > 0) {
@@ -1831,7 +1845,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_
         const int row = lane >> 3;
         const bool aligned = (P.width & 3) == 0 && ((size_t)P.colors & 3) == 0;
         const bool packed = aligned && ((full >> (row * 8)) & 0xffull) == 0xffull;
-        unsigned char *rowBytes = sSkyRow[threadIdx.x >> 6][row];
+        unsigned char *rowBytes = sSkyRow[lw][row];
         if (packed) {
             rowBytes[3 * (lane & 7)] = c0;
             rowBytes[3 * (lane & 7) + 1] = c1;
@@ -1842,10 +1856,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_SKY_
             const int rr = lane / 6, dw = lane - rr * 6;
             if (aligned && ((full >> (rr * 8)) & 0xffull) == 0xffull) {
                 /* this row's first pixel: column 0 of the tile, row rr */
-                const int x0 = blockIdx.x * kTileW + ((threadIdx.x >> 6) & 1) * 8;
-                const int r0 = blockIdx.y * kTileH + ((threadIdx.x >> 6) >> 1) * 8 + rr;
+                const int x0 = bx * kTileW + (w16 & 1) * 8;
+                const int r0 = by * kTileH + (w16 >> 1) * 8 + rr;
                 unsigned *dst = (unsigned *)(P.colors + 3 * ((size_t)r0 * (size_t)P.width + (size_t)x0));
-                dst[dw] = ((const unsigned *)sSkyRow[threadIdx.x >> 6][rr])[dw];
+                dst[dw] = ((const unsigned *)sSkyRow[lw][rr])[dw];
             }
         }
         if (px.valid) {
@@ -3040,7 +3054,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky0, skyStream));
-            hipLaunchKernelGGL(rtc_render_sky, grid, dim3(kBlock), 0, skyStream, P, (const unsigned *)tileW);
+            if (smallShare && (size_t)d->width * (size_t)rows > 400000)
+                hipLaunchKernelGGL(rtc_render_sky<4>, grid, dim3(256), 0, skyStream, P, (const unsigned *)tileW);
+            else
+                hipLaunchKernelGGL(rtc_render_sky<1>, dim3(grid.x * 2, grid.y * 2), dim3(64), 0, skyStream, P,
+                                   (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky1, skyStream));
