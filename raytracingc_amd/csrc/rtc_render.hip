@@ -1907,7 +1907,10 @@ constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the def
 #define RTC_INLINE_SUM_PIXELS 600000
 #endif
 constexpr size_t kInlineSumPixels = RTC_INLINE_SUM_PIXELS;
-constexpr int kChainBlock = 256;
+#ifndef RTC_CHAIN_BLOCK
+#define RTC_CHAIN_BLOCK 256
+#endif
+constexpr int kChainBlock = RTC_CHAIN_BLOCK; /* threads per chain workgroup */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
  * in the chain kernel's idle issue slots instead of waiting for its tail, and the launch stream's small kernels are no
