@@ -211,6 +211,7 @@ struct RtcDeviceScene {
     hipEvent_t evCullSync; /* the launch stream's position when the culls move to `cst` */
     bool skyPending[kSkySlots];
     SkyKey skyKey[kSkySlots];
+    unsigned long long skySeq[kSkySlots], skyCount; /* enqueue order of the sky passes (skySeq[h] of slot h's) */
     hipEvent_t evSkyDone[kSkySlots], evGeoDone[kSkySlots];
     hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
     /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
@@ -2898,23 +2899,30 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
      * overlapped launch waits when a pending pass reads the slot it rewrites, or writes the same Color or
      * accumulator buffer with other rows, camera or environment (the same ones write the same sky pixels with the
-     * same values, and never a pixel this launch's geometry kernel writes).  One wait, on the newest pass, covers
-     * every earlier one (the side stream runs them in order), so with kSkySlots slots a pipelined sequence of one
-     * camera waits once every kSkySlots - 1 launches: each wait is a cross-stream hop of ~10 us before the next
-     * kernel (round 3: waiting before every geometry kernel cost 0.107 vs 0.098 ms per 1080p 1/8 share). */
+     * same values, and never a pixel this launch's geometry kernel writes).  One wait, on the newest such pass,
+     * covers every earlier one (the side stream runs them in order), so with kSkySlots slots a pipelined sequence of
+     * one camera waits once every kSkySlots - 1 launches: each wait is a cross-stream hop of ~10 us before the next
+     * kernel (round 3: waiting before every geometry kernel cost 0.107 vs 0.098 ms per 1080p 1/8 share).  Round 4
+     * waits for the newest CONFLICTING pass, not the newest pass: a moving camera's pipelined frames into three
+     * buffers conflict with the pass three launches back, long finished, and no longer wait for the previous frame's
+     * sky pass (which serialised them behind it). */
     const SkyKey key = sky_key(P);
-    bool mustWait = false;
+    int waitSky = -1; /* the newest pending pass this launch must wait for */
     for (int h = 0; h < kSkySlots; ++h)
-        if (s->skyPending[h]) /* (with `cs` the cull stream waits for the pass reading its slot itself, below) */
-            mustWait = mustWait || !overlap || (h == half && cs == st) ||
-                       ((s->skyKey[h].colors == key.colors || (key.accum && s->skyKey[h].accum == key.accum)) &&
-                        memcmp(&s->skyKey[h], &key, sizeof key) != 0);
-    if (mustWait) {
-        HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[s->lastSky], 0));
+        if (s->skyPending[h] && /* (with `cs` the cull stream waits for the pass reading its slot itself, below) */
+            (!overlap || (h == half && cs == st) ||
+             ((s->skyKey[h].colors == key.colors || (key.accum && s->skyKey[h].accum == key.accum)) &&
+              memcmp(&s->skyKey[h], &key, sizeof key) != 0)) &&
+            (waitSky < 0 || s->skySeq[h] > s->skySeq[waitSky]))
+            waitSky = h;
+    if (waitSky >= 0) {
+        HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[waitSky], 0));
         if (chainOnCs) /* the geometry kernel writes Color rows on `cs` */
-            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[s->lastSky], 0));
-        for (int h = 0; h < kSkySlots; ++h)
-            ms->skyPending[h] = false;
+            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[waitSky], 0));
+        const unsigned long long upTo = s->skySeq[waitSky];
+        for (int h = 0; h < kSkySlots; ++h) /* that pass and every earlier one are done before this launch's kernels */
+            if (s->skySeq[h] <= upTo)
+                ms->skyPending[h] = false;
     }
     size_t halfBytes = 0;
     if (cull) {
@@ -3071,6 +3079,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
                 ms->skyPending[half] = true;
                 ms->skyKey[half] = key;
+                ms->skySeq[half] = ++ms->skyCount;
                 ms->lastSky = half;
             }
             if (s->timing)
