@@ -188,8 +188,8 @@ struct RtcDeviceScene {
     size_t scratchCap; /* bytes */
     /* RTC_F_OVERLAP: launches cycle through kSkySlots slots of the scratch; skyPending[h]: a sky pass that reads
      * slot h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends; skyKey[h]: the rows,
-     * camera and environment it writes); lastSky: the slot of the newest one */
-    int flip, lastSky;
+     * camera and environment it writes; skySeq[h]: its enqueue order) */
+    int flip;
     /* rtc_render_chain's sub-list counters: a ring of kGeoRing sets, set q % kGeoRing for the q-th split launch;
      * each launch's tile cull zeroes the next launch's set, so a launch on the same stream as the previous one
      * needs no rtc_prep_primary to clear its counters (cullStream: that stream) */
@@ -3080,7 +3080,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 ms->skyPending[half] = true;
                 ms->skyKey[half] = key;
                 ms->skySeq[half] = ++ms->skyCount;
-                ms->lastSky = half;
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, gs));
