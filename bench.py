@@ -229,6 +229,30 @@ def kernel_roofline(name, live_ms, dg, work):
     return e
 
 
+def frame_roofline(dg, frame_s):
+    """The whole frame against both bounds: the VALU issue slots of every kernel of one frame (the
+    digest's per-dispatch counters, one dispatch each) over what 1024 SIMDs issue at 2.4 GHz in ms_per_step, and the
+    counter HBM bytes of those dispatches per frame against HBM_PEAK_GBS."""
+    ks = (dg or {}).get("kernels") or {}
+    if not ks or not frame_s:
+        return None
+    slots = bytes_ = 0.0
+    names = []
+    for name, k in sorted(ks.items()):
+        pd = k.get("per_dispatch", {})
+        if "SQ_INSTS_VALU" not in pd and "traffic_bytes" not in k:
+            continue
+        names.append(name)
+        f64 = sum(pd.get(c, 0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        slots += 2.0 * pd.get("SQ_INSTS_VALU", 0) + 2.0 * f64
+        bytes_ += k.get("traffic_bytes", 0)
+    gbs = bytes_ / frame_s / 1e9
+    return {"kernels": names, "valu_issue_frac": round(slots / (1024 * 2.4e9 * frame_s), 4),
+            "bytes_per_frame": int(bytes_), "hbm_gbs": round(gbs, 2), "hbm_peak_gbs": HBM_PEAK_GBS,
+            "hbm_frac": round(gbs / HBM_PEAK_GBS, 5), "source": dg.get("source")}
+
+
 # ---- GPU ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -251,7 +275,7 @@ def main():
     import torch.distributed as dist
 
     import raytracingc_amd as rt
-    from raytracingc_amd.distributed import SharedHostFrames, rank_config, rows_per_rank
+    from raytracingc_amd.distributed import SharedHostFrames, pin_rank_near_gpu, rank_config, rows_per_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -265,6 +289,8 @@ def main():
                          f"--backend gloo for a rehearsal with ranks sharing GPUs")
     gpu = local % ndev
     torch.cuda.set_device(gpu)
+    # N > 1: the ranks share the node's CPU quota -- one intra-op thread each, pinned near their GPU when allowed
+    pinning = pin_rank_near_gpu(gpu) if multi else None
     dev = torch.device("cuda", gpu)
     n_phys = min(world, ndev)  # distinct GPUs the ranks run on (one node)
     backend = None
@@ -450,6 +476,7 @@ def main():
         # the line's top-level roofline: the dominant kernel against its VALU issue bound (no MFMA, no HBM bound)
         frac = dk.get("valu_issue_frac")
         bf_tf = seg_traced / world * T * FLOPS_PER_TEST / (t / args.steps) / 1e12
+        frame_roof = frame_roofline(dg, t / args.steps)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -480,6 +507,10 @@ def main():
                          "achieved": dk.get("valu_issue_frac"), "peak": 1.0, "unit": "VALU issue fraction",
                          "frac": frac, "frac_isolated": dk.get("valu_issue_frac_isolated"),
                          "traffic": dk.get("traffic"),
+                         # SURVEY §8(d)'s own contract: executed ray-triangle tests x 57 flop over the chain kernel's
+                         # time against the FP32 vector peak
+                         "frac_57flop": (chain_work or {}).get("frac_57flop"),
+                         "frame": frame_roof,
                          "kernels": kernels,
                          "bruteforce_equiv_tflops": round(bf_tf, 3),
                          "note": "per kernel: ms = HIP events around it on its own stream (live); valu_issue_frac = "
@@ -489,7 +520,9 @@ def main():
                                  "the committed rocprofv3 PMC digest of this workload (roofline.kernels.*.source); "
                                  "frac_57flop = ray-triangle tests x 57 flop / ms / 157.3 TFLOP/s (SURVEY §8 d); "
                                  "traffic = counter HBM bytes per launch (traffic_note: which correction); "
-                                 "bruteforce_equiv = segments x T x 57 per frame time, not a roofline"},
+                                 "bruteforce_equiv = segments x T x 57 per frame time, not a roofline; frame = every "
+                                 "kernel of one frame (the digest's per-dispatch counters) over ms_per_step: VALU issue "
+                                 "and counter HBM bytes against 8 TB/s (north_star's HBM roofline fraction)"},
             "frame_ms": round(t / args.steps * 1e3, 4),
             "frame_loop": {"enqueue_ms_per_frame": round(lst["enqueue_ms"] / max(1, lst["frames"]), 4),
                            "copy_ms_median": round(lst["copy_ms_median"], 4), "copy_ms_max": round(lst["copy_ms_max"], 4),
@@ -506,6 +539,7 @@ def main():
         ref1, gacc, _ = rt.render(tris, None, scene, cam, cfg_joined, device=gpu, want_accum=(world == 1))
         line["host_frame_equals_rtc_render"] = bool(np.array_equal(frame_host, ref1))
         if multi:
+            line["rank_cpu"] = pinning
             line["ranks"] = world
             line["ranks_per_gpu"] = round(world / n_phys, 3)
             line["rehearsal"] = backend == "gloo"

@@ -91,11 +91,12 @@ typedef struct RtcRenderDesc {
                                      first kernel.  Every overlapped launch but a row-stride-1 frame of at most
                                      600 k pixels prepares, culls and runs its geometry kernel on one of two scene
                                      streams (alternating), unordered against the previous launch's geometry
-                                     kernel, and sums each pixel's samples in-kernel; `stream` waits for that kernel at the
-                                     launch's end, not for the sky pass.  The
-                                     frame is complete when the scene's frame event (rtc_scene_set_frame_event)
-                                     fires; with segment counters requested the launch joins as usual.  Same
-                                     frame bit for bit. */
+                                     kernel, and sums each pixel's samples in-kernel: such a launch starts after
+                                     everything enqueued on `stream` before it, but `stream` is not made to wait for
+                                     its kernels.  Every overlapped launch's frame is complete when the scene's frame
+                                     event (rtc_scene_set_frame_event) fires -- consume it there, not at `stream`;
+                                     with segment counters requested the launch joins as usual.  Same frame bit for
+                                     bit. */
 
 typedef struct RtcStats {
     double renderMs;             /* device time of the render launch (slowest device), HIP events */

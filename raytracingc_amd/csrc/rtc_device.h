@@ -11,6 +11,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+/* Timing-experiment switches that change the frame (not the reference's arithmetic): a build defines one only together
+ * with RTC_EXPERIMENT, which the Makefile's product targets never define. */
+#if (defined(RTC_AB_CHEAP_ENV_SKY) || defined(RTC_AB_CHEAP_ENV_CHAIN) || defined(RTC_AB_CHEAP_DIR) ||                 \
+     defined(RTC_AB_NO_BM_FALLBACK) || defined(RTC_AB_NO_SLOTS)) && !defined(RTC_EXPERIMENT)
+#error "RTC_AB_* switches produce a wrong frame (timing experiments only): define RTC_EXPERIMENT as well"
+#endif
+
 #include "rtc_math.h"
 
 namespace rtcdev {

@@ -729,7 +729,10 @@ extern "C" int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void
             if (hsa_amd_memory_async_copy((char *)dst + (size_t)r * hostPitch, cpu, (const char *)devSrc + (size_t)r * srcPitch,
                                           gpu, rowBytes, 0, nullptr, sig.s) != HSA_STATUS_SUCCESS) {
                 hsa_signal_subtract_screlease(sig.s, rows - r); /* the copies not issued */
-                (void)dma_wait(sig.s, hostDst, span, devSrc, srcSpan, "rtc_copy_rows_d2h_dma");
+                /* drain the copies already issued; if that wait timed out they may still write hostDst: report
+                 * RTC_ETIMEDOUT (rtc_dma_pending lists them), not RTC_EIO */
+                if (int wrc = dma_wait(sig.s, hostDst, span, devSrc, srcSpan, "rtc_copy_rows_d2h_dma"))
+                    return wrc;
                 return rtc_fail(RTC_EIO, "rtc_copy_rows_d2h_dma: hsa_amd_memory_async_copy failed (row %d)", r);
             }
     }

@@ -2893,7 +2893,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     }
     hipStream_t cs = chainOnCs ? ((half & 1) ? s->cst2 : s->cst) : overlap && smallShare && RTC_CULL_STREAM ? s->cst : st;
     hipStream_t gs = chainOnCs ? cs : st; /* the geometry kernel's stream */
-    const bool altStreams = chainOnCs && (s->cullStream == s->cst || s->cullStream == s->cst2);
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
      * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
      * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
@@ -2916,9 +2915,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             (waitSky < 0 || s->skySeq[h] > s->skySeq[waitSky]))
             waitSky = h;
     if (waitSky >= 0) {
+        /* evSkyDone[h] fires once launch h's sky pass AND its geometry kernel have ended (the side stream records it
+         * after waiting for evGeoDone[h]); `cs` inherits this wait through the caller-position event below */
         HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[waitSky], 0));
-        if (chainOnCs) /* the geometry kernel writes Color rows on `cs` */
-            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[waitSky], 0));
         const unsigned long long upTo = s->skySeq[waitSky];
         for (int h = 0; h < kSkySlots; ++h) /* that pass and every earlier one are done before this launch's kernels */
             if (s->skySeq[h] <= upTo)
@@ -2998,24 +2997,28 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * a 5 us kernel at the head of every frame) */
     const float org[3] = {P.origin.x, P.origin.y, P.origin.z};
     if (cs != st) {
-        /* the cull stream rewrites slot `half`: after the earlier launch that used it (its sky pass and its
-         * launch-stream kernels), and after the launch stream's current position when the culls move over from it
-         * (a cull enqueued there may still zero this launch's counter set) */
+        /* The cull stream runs this launch's first kernels, so it starts after everything the caller enqueued on `st`
+         * before the launch (e.g. a wait for the previous consumer of this Color buffer) and after the sky waits above:
+         * an event at `st`'s current position.  `st` carries nothing of earlier launches on the cull streams (they do
+         * not make it wait for their geometry kernels), so this orders no geometry kernel after another.  Then slot
+         * `half`: the earlier launch that used it must have ended (its sky pass and geometry kernel) */
+        HIP_TRY(hipEventRecord(s->evCullSync, st));
+        HIP_TRY(hipStreamWaitEvent(cs, s->evCullSync, 0));
         if (s->slotUsed[half]) {
             HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[half], 0));
             HIP_TRY(hipStreamWaitEvent(cs, s->evGeoDone[half], 0));
         }
-        if (altStreams) {
-            /* the previous launch's cull (the other cull stream) zeroes this launch's counter set */
-            HIP_TRY(hipStreamWaitEvent(cs, s->evFork, 0));
-        } else if (s->cullStream != cs) {
-            HIP_TRY(hipEventRecord(s->evCullSync, st));
-            HIP_TRY(hipStreamWaitEvent(cs, s->evCullSync, 0));
-        }
     }
+    /* the previous split launch's tile cull zeroes this launch's counter set (P.geoCountNext): when it ran on another
+     * stream (the other cull stream, a cull stream before a launch on `st`, another caller stream), wait for it --
+     * evFork is its completion (only split launches record it, and only they touch the counter sets) */
+    if (chain && s->cullStream && s->cullStream != cs)
+        HIP_TRY(hipStreamWaitEvent(cs, s->evFork, 0));
     const bool prepCurrent =
         s->prepValid[half] && s->prepStream[half] == cs && memcmp(s->prepOrigin[half], org, sizeof org) == 0;
-    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || altStreams));
+    /* the previous split launch's cull zeroed this launch's counter set, and `cs` is ordered after it (same stream, or
+     * the evFork wait above) */
+    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || RTC_SIDE_STREAM));
     /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
      * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
     if (chain)
@@ -3075,8 +3078,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evSky1, skyStream));
             if (RTC_SIDE_STREAM)
                 HIP_TRY(hipEventRecord(s->evJoin, s->side));
-            if (overlap) { /* this sky pass reads scratch slot `half` until evSkyDone[half] */
-                HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
+            if (overlap) { /* this sky pass reads scratch slot `half` until evSkyDone[half] (recorded below) */
                 ms->skyPending[half] = true;
                 ms->skyKey[half] = key;
                 ms->skySeq[half] = ++ms->skyCount;
@@ -3119,10 +3121,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             ms->timed = s->timing;
             if (overlap) {
                 /* no join: the frame is complete once the side stream has passed both passes (evGeoDone: recorded
-                 * by the last kernel above) */
+                 * by the last kernel above).  evSkyDone[half] marks that point too, so a later launch that waits for
+                 * this one (a conflicting buffer, the slot's reuse, a joined launch) waits for its geometry kernel as
+                 * well, wherever that ran (on the cull streams it is not ordered before the side stream's
+                 * sky pass).  `st` is not made to wait: with the geometry kernel on a cull stream the next launch's
+                 * cull stream waits for `st`'s position, which would order that geometry kernel after this one */
                 HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone[half], 0));
-                if (chainOnCs) /* the launch stream holds the geometry pass too */
-                    HIP_TRY(hipStreamWaitEvent(st, s->evGeoDone[half], 0));
+                HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
                 if (frameEvent)
                     HIP_TRY(hipEventRecord(frameEvent, s->side));
                 ms->slotUsed[half] = true;

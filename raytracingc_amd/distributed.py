@@ -21,6 +21,54 @@ import torch.distributed as dist
 from . import RenderConfig, deinterleave_async
 
 
+def parse_cpulist(text: str) -> set[int]:
+    """A sysfs CPU list ("0-3,8,10-11") as a set of CPU numbers."""
+    cpus: set[int] = set()
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def gpu_local_cpus(device_index: int) -> set[int] | None:
+    """The CPUs of the NUMA node nearest GPU `device_index` (its PCI device's local_cpulist), or None when the
+    properties or sysfs do not say."""
+    try:
+        props = torch.cuda.get_device_properties(device_index)
+        bus = "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), props.pci_bus_id, props.pci_device_id)
+        with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+            cpus = parse_cpulist(f.read())
+        return cpus or None
+    except Exception:
+        return None
+
+
+def pin_rank_near_gpu(device_index: int, threads: int = 1) -> dict:
+    """Per-rank CPU hygiene for N ranks on one node: cap torch's intra-op threads (the ranks share the
+    box's CPU quota; a rank's host work is the launch enqueue and one copy thread that blocks on HSA signals) and, when
+    the affinity mask allows, pin the process to the CPUs nearest its GPU.  Returns what was done."""
+    import os
+
+    done = {"torch_threads": threads}
+    torch.set_num_threads(threads)
+    try:
+        allowed = os.sched_getaffinity(0)
+    except AttributeError:
+        return done
+    near = gpu_local_cpus(device_index)
+    pick = (near & allowed) if near else set()
+    if pick and pick != allowed:
+        try:
+            os.sched_setaffinity(0, pick)
+            done["cpus"] = len(pick)
+        except OSError:
+            pass
+    return done
+
+
 def rows_per_rank(height: int, world: int) -> int:
     """Rows in the largest part (rank 0's); every rank's compact buffer is padded to this for the gather."""
     return (height + world - 1) // world

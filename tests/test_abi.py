@@ -152,3 +152,22 @@ def test_ctypes_signatures_match_header():
             assert len(at) == n, f"{name}: {len(at)} argtypes, header declares {n} parameters"
             checked += 1
     assert checked >= 25
+
+
+@pytest.mark.parametrize("switch", ["RTC_AB_CHEAP_DIR", "RTC_AB_CHEAP_ENV_SKY", "RTC_AB_NO_SLOTS"])
+def test_experiment_switches_need_rtc_experiment(switch):
+    """the RTC_AB_* timing switches change the frame, so the device sources refuse to compile with one
+    unless RTC_EXPERIMENT is defined too (the Makefile's product targets never define it)."""
+    import shutil
+    import subprocess
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    src = os.path.join(REPO, "raytracingc_amd", "csrc", "rtc_render.hip")
+    base = [hipcc, "--offload-arch=gfx950", "-std=c++17", "-E", src, "-o", os.devnull]
+    bad = subprocess.run(base + ["-D" + switch], capture_output=True, text=True, timeout=300)
+    assert bad.returncode != 0 and "RTC_EXPERIMENT" in bad.stderr
+    ok = subprocess.run(base + ["-D" + switch, "-DRTC_EXPERIMENT"], capture_output=True, text=True, timeout=300)
+    assert ok.returncode == 0, ok.stderr[-500:]
+    assert "RTC_EXPERIMENT" not in open(os.path.join(REPO, "Makefile")).read()

@@ -116,6 +116,13 @@ def test_gloo_subgroup_without_global_rank0():
     assert np.array_equal(frame, full.numpy())
 
 
+def test_parse_cpulist():
+    from raytracingc_amd.distributed import parse_cpulist
+
+    assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert parse_cpulist("") == set() and parse_cpulist("5") == {5}
+
+
 def test_partition_helpers():
     import raytracingc_amd as rt
 
@@ -140,6 +147,10 @@ def _shared_worker(rank, world, port, q, name):
     try:
         import raytracingc_amd as rt
 
+        from raytracingc_amd.distributed import pin_rank_near_gpu
+
+        pin_rank_near_gpu(0)  # (no GPU here: caps the threads and leaves the affinity alone)
+        assert torch.get_num_threads() == 1
         frames = SharedHostFrames(name, 2, H, W, rank, dist.barrier, register=False)
         cfg = rank_config(rt.RenderConfig(W, H, SPP, 10, True), rank, world)
         part = torch.zeros((rows_per_rank(H, world), W, 3), dtype=torch.uint8)
@@ -159,10 +170,10 @@ def _shared_worker(rank, world, port, q, name):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_shared_host_frame_rows(world):
     """The multi-process host-frame layout: every rank's interleaved rows land in one shared frame that equals the
-    single-process frame (SharedHostFrames, bench.py at N > 1)."""
+    single-process frame (SharedHostFrames, bench.py at N > 1); world 8 is the node the driver's scaling run uses."""
     import raytracingc_amd as rt
 
     ctx = mp.get_context("spawn")

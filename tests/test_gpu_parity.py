@@ -346,25 +346,30 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     ds.close()
 
 
+@pytest.mark.parametrize("size", [(256, 144, 8), (1920, 1080, 4)])
 @pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}])
-def test_overlapped_frames_bit_exact(variant, gpu_available):
+def test_overlapped_frames_bit_exact(variant, size, gpu_available):
     """RTC_F_OVERLAP (frame pipelining): launches that do not join their sky pass, with the next launch's
-    preparation (tile cull into the other scratch half) overlapping it.  Eight frames over three cameras, each
-    consumed (copied) once its frame event fires, and two frames of different cameras into one buffer: every
-    frame equals a joined rtc_render bit for bit (with each geometry-pixel kernel)."""
+    preparation (tile cull into the other scratch slot) overlapping it.  Eight frames over three cameras into two
+    buffers, each consumed (copied, after a delay on the consumer's stream) once its frame event fires and rewritten
+    only after the launch stream waited for that copy, and two frames of different cameras into one buffer: every
+    frame equals a joined rtc_render bit for bit.  At 1920x1080 the launches run on the alternating cull streams
+    (they must still start after the caller's wait on the launch stream, and a conflicting launch must
+    wait for the previous launch's geometry kernel, not only for its sky pass)."""
     import torch
 
     tris, _ = load_tris("ultracomplex")
     scene = rt.default_scene()
     cams = [rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1),
             rt.camera_basis((-5.3, -1.2, -4.1), (1.2, -1.4, 0.7), 0.9)]
-    W, H, spp = 256, 144, 8
+    W, H, spp = size
     ref = [rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))[0] for c in cams]
     cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True, **variant)
     ds = rt.DeviceScene(tris, None)
     st, cp = torch.cuda.Stream(), torch.cuda.Stream()
-    bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
-    freed = [None] * 3
+    nb = 2
+    bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    freed = [None] * nb
     got = []
     def new_event():  # a torch event has no hipEvent_t until its first record
         e = torch.cuda.Event()
@@ -372,7 +377,7 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
         return e
 
     for k in range(8):
-        b = k % 3
+        b = k % nb  # buffer b sees cameras 0, 2, 1, 0 ... : a frame written too early is detected
         if freed[b] is not None:  # buffer b is rewritten only after its previous frame was copied
             st.wait_event(freed[b])
         ev = new_event()
@@ -380,6 +385,8 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
         ds.render_rows_async(scene, cams[k % 3], cfg, bufs[b].data_ptr(), stream=st.cuda_stream)
         cp.wait_event(ev)
         with torch.cuda.stream(cp):
+            if hasattr(torch.cuda, "_sleep"):
+                torch.cuda._sleep(2_000_000)  # ~1 ms: the copy runs late, the next frame's kernels are queued by then
             got.append(bufs[b].clone())
             freed[b] = torch.cuda.Event()
             freed[b].record(cp)
@@ -387,8 +394,8 @@ def test_overlapped_frames_bit_exact(variant, gpu_available):
     for k, g in enumerate(got):
         assert np.array_equal(g.cpu().numpy(), ref[k % 3]), f"frame {k}"
     # one buffer, two cameras back to back: the second frame's geometry pixels are not overwritten by the first
-    # frame's late sky pass
-    for c in (cams[1], cams[2]):
+    # frame's late sky pass or geometry kernel
+    for c in (cams[1], cams[2], cams[0], cams[2]):
         ev = new_event()
         ds.set_frame_event(ev.cuda_event)  # one-shot: armed for each launch
         ds.render_rows_async(scene, c, cfg, bufs[0].data_ptr(), stream=st.cuda_stream)
@@ -429,15 +436,18 @@ def test_overlap_slot_ring(gpu_available):
     ds.close()
 
 
-def test_overlap_with_counters_and_mixed_launches(gpu_available):
+@pytest.mark.parametrize("size", [(200, 120, 6), (1920, 1080, 2)])
+def test_overlap_with_counters_and_mixed_launches(size, gpu_available):
     """An RTC_F_OVERLAP launch that asks for segment counters joins (the counts equal a joined launch's), and
-    joined / overlapped / no-tile-cull launches interleaved on one scene (the scratch halves and pending sky
-    passes) each produce their frame bit for bit."""
+    joined / overlapped / no-tile-cull launches interleaved on one scene (the scratch slots and pending sky
+    passes) each produce their frame bit for bit.  At 1920x1080 the overlapped launches run on the alternating cull
+    streams, so the joined launch after them and the overlapped launch after that cross streams both ways (ADVICE r04:
+    a joined launch's scratch slot 0 must not be rewritten under it by the next cull stream launch)."""
     import torch
 
     tris, _ = load_tris("complex")
     scene, cam, _ = setup_from_flags({})
-    W, H, spp = 200, 120, 6
+    W, H, spp = size
     ref, _, st = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))
     ds = rt.DeviceScene(tris, None)
     s = torch.cuda.current_stream()

@@ -20,7 +20,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 root, workload = sys.argv[1], sys.argv[2]
-KERNELS = ("rtc_render_chain", "rtc_render_sky", "rtc_accumulate_samples", "rtc_tile_cull", "rtc_prep_primary")
+KERNELS = ("rtc_render_chain", "rtc_render_sky", "rtc_accumulate_samples", "rtc_tile_cull", "rtc_super_cull",
+           "rtc_prep_primary")
 
 
 def short(name):
