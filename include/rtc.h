@@ -45,7 +45,11 @@ typedef struct RtcCamera { vec3 origin, ex, ey, ez; float fov; } RtcCamera;   /*
 /* Which pixels and how.  width/height/maxBounce = main.c:10-12; spp = accumulationCount (scene.h:26);
  * trianglesOnly = main.c:113,241.  Rows rendered: y = rowStart + k*rowStride for k = 0..ceil(..)-1, the
  * reference's row interleave (main.c:84) lifted to devices/ranks.  rowStride = 1, rowStart = 0 renders the
- * whole frame. */
+ * whole frame.  rowBand = B > 1 (a power of two, at most 64; 0 or 1: single rows) interleaves bands of B rows
+ * instead: launch row r is image row y = rowStart + (r / B)*rowStride*B + r % B -- rank g of G renders the bands
+ * b = g, g + G, ... with rowStart = g*B, rowStride = G (north_star's row-tile split: with B = 8 a rank's 8x8 pixel
+ * tiles are 8 adjacent image rows, not 8 rows G apart).  The launch writes its rows compactly in that order.  The
+ * frame does not depend on the partition (the seed is the absolute pixel index, main.c:95). */
 typedef struct RtcRenderDesc {
     int width, height;
     int spp;
@@ -53,6 +57,7 @@ typedef struct RtcRenderDesc {
     int trianglesOnly;
     int rowStart, rowStride;
     int flags;                 /* RTC_F_* */
+    int rowBand;               /* rows per interleaved band (0 or 1: single rows) */
 } RtcRenderDesc;
 
 #define RTC_F_HOIST_PRIMARY 0x1  /* bit-exact: trace each pixel's primary ray once; default off */
@@ -155,7 +160,8 @@ int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sp
 
 /* Single-process multi-GPU variant of rtc_render (replaces the 12-pthread fan-out main.c:285-302): devices
  * 0..numDevices-1 each render the rows y = g + k*numDevices (the reference's row interleave, main.c:84,
- * lifted to GPUs) into a compact part, concurrently; one RCCL communicator clique (ncclCommInitAll) gathers
+ * lifted to GPUs) -- or, with d->rowBand = B > 1, the bands of B rows b = g + k*numDevices -- into a compact part,
+ * concurrently; one RCCL communicator clique (ncclCommInitAll) gathers
  * the parts to device 0 over xGMI (ncclGather, grouped), device 0 re-interleaves them and one D2H brings the
  * frame to the host.  Output is bit-identical to numDevices = 1 (the seed is the absolute pixel index,
  * main.c:95).  RCCL errors are returned as positive ncclResult_t values.  stats->renderMs = slowest
@@ -169,7 +175,8 @@ typedef struct RtcDeviceScene RtcDeviceScene;
 int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                      int device, RtcDeviceScene **out);
 int rtc_scene_release(RtcDeviceScene *s);
-/* Number of rows d selects: ceil((height - rowStart) / rowStride), 0 if none. */
+/* Number of rows d selects (ceil((height - rowStart) / rowStride) for single rows; with bands, the full bands' rows
+ * plus the last band's rows inside the frame), 0 if none. */
 int rtc_rows_selected(const RtcRenderDesc *d);
 /* Asynchronous on `stream` (a hipStream_t, NULL = default stream).  dColors: device buffer of
  * rows_selected*width*3 bytes; dAccum: nullable device float buffer rows_selected*width*3; dSegments:
@@ -241,7 +248,8 @@ int rtc_host_unregister(void *p);
 /* Pipelined frames on one device, driven from native code (the per-frame host cost is the launch enqueue alone).
  * Frame k renders d's rows with RTC_F_OVERLAP into devRows[k % nbuf] (device buffers of rows_selected*width*3 bytes)
  * on `stream`; a copy thread waits for the frame's event and moves the rows into hostRows[k % nbuf] (page-locked,
- * row pitch hostPitch) with rtc_copy_rows_d2h_dma; buffer b is rendered into again once its copy has finished.
+ * pitch hostPitch between consecutive rows, or between consecutive bands of d->rowBand rows, each band's rows
+ * adjacent) with rtc_copy_rows_d2h_dma; buffer b is rendered into again once its copy has finished.
  * Returns when the last frame's rows are in host memory.  Uses the scene's frame event hook itself. */
 typedef struct RtcLoopStats {
     double wallMs;       /* first enqueue .. the last frame's rows in host memory (host clock) */
@@ -266,6 +274,10 @@ int rtc_frame_loop_cameras(RtcDeviceScene *s, const Scene *scene, const RtcCamer
  * g holding rows y = g + k*parts; dOut receives the height*width*3 frame.  Asynchronous on `stream`. */
 int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,
                            void *dOut, void *stream);
+/* The same for parts of interleaved bands of rowBand rows (RtcRenderDesc.rowBand; 0 or 1: single rows): block g holds
+ * the bands b = g, g + parts, ... (rows b*rowBand .. b*rowBand + rowBand - 1), each band's rows in order. */
+int rtc_deinterleave_bands_async(const void *dCompact, int parts, int rowsPerPart, int width, int height, int rowBand,
+                                 void *dOut, void *stream);
 
 /* ---- device probes: run single reference functions on the GPU for known-answer tests --------------- */
 /* Each copies inputs to the current device, runs one kernel of the same device code the renderer uses,

@@ -247,6 +247,14 @@ typedef struct {
     unsigned long long segments;
 } OThread;
 
+/* Launch row r -> image row y (rtc.h RtcRenderDesc): rows y = rowStart + k*rowStride (main.c:84's interleave), or with
+ * rowBand B > 1 bands of B rows, band k starting at rowStart + k*rowStride*B */
+static int oracle_row_y(const RtcRenderDesc *d, int r)
+{
+    const int B = d->rowBand > 1 ? d->rowBand : 1;
+    return d->rowStart + (r / B) * d->rowStride * B + r % B;
+}
+
 static void *o_row_thread(void *p)
 {
     OThread *a = p;
@@ -254,7 +262,7 @@ static void *o_row_thread(void *p)
     const int width = d->width, height = d->height;
     const float invSpp = (float)(1. / (double)d->spp);
     for (int r = a->tid; r < a->rows; r += a->nthreads) {
-        int y = d->rowStart + r * d->rowStride;
+        int y = oracle_row_y(d, r);
         for (int x = 0; x < width; ++x) {
             float dx = (x - width / 2) / (float)(height / 2);
             float dy = (y - (height / 2)) / (float)(height / 2);
@@ -287,9 +295,11 @@ static void *o_row_thread(void *p)
 /* ---- exported -------------------------------------------------------------------------------------- */
 int oracle_rows_selected(const RtcRenderDesc *d)
 {
-    if (d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height)
+    if (d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height || d->rowBand < 0)
         return 0;
-    return (d->height - d->rowStart + d->rowStride - 1) / d->rowStride;
+    const int B = d->rowBand > 1 ? d->rowBand : 1, step = d->rowStride * B;
+    const int nb = (d->height - d->rowStart + step - 1) / step, last = d->rowStart + (nb - 1) * step;
+    return (nb - 1) * B + (d->height - last < B ? d->height - last : B);
 }
 
 /* The render seam main.c:263-304 on the CPU: same arguments as rtc_render, plus the thread count. */

@@ -135,6 +135,9 @@ class RenderConfig:
     hoist: bool = False
     row_start: int = 0
     row_stride: int = 1
+    # rows per interleaved band (rtc.h rowBand): 0/1 single rows y = row_start + k*row_stride; B > 1 (a power of two)
+    # bands of B rows starting at row_start + k*row_stride*B
+    row_band: int = 0
     debug_bounces: bool = False  # calcDebugColor (raytracing.c:242-260) instead of calcColor
     tile_cull: bool = True  # primary segments visit their 8x8 tile's candidate triangles (bit-exact)
     reorder: bool = True  # dispatch the workgroups that see geometry first (same frame)
@@ -157,7 +160,7 @@ class RenderConfig:
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),
-                             self.row_start, self.row_stride, self.flags())
+                             self.row_start, self.row_stride, self.flags(), self.row_band)
 
     def rows(self) -> int:
         d = self.desc()
@@ -329,7 +332,13 @@ def dma_pending(ptr: int | None = None, nbytes: int = 0) -> int:
 
 
 def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: int, height: int, out_ptr: int,
-                       stream: int | None = None):
+                       stream: int | None = None, row_band: int = 1):
+    """rtc_deinterleave_async (single rows) / rtc_deinterleave_bands_async (bands of row_band rows)."""
+    if row_band > 1:
+        check(lib().rtc_deinterleave_bands_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height, row_band,
+                                                 C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
+              "rtc_deinterleave_bands_async")
+        return
     check(lib().rtc_deinterleave_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height,
                                        C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
           "rtc_deinterleave_async")

@@ -61,6 +61,7 @@ class RtcRenderDesc(C.Structure):
         ("rowStart", C.c_int),
         ("rowStride", C.c_int),
         ("flags", C.c_int),
+        ("rowBand", C.c_int),  # rows per interleaved band (rtc.h; 0 or 1: single rows)
     ]
 
 
@@ -136,7 +137,7 @@ EXPORTS = [
     "rtc_render", "rtc_render_multi",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
-    "rtc_deinterleave_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
+    "rtc_deinterleave_async", "rtc_deinterleave_bands_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
     "rtc_host_unregister", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
@@ -205,6 +206,8 @@ def lib() -> C.CDLL:
     L.rtc_render_rows_async.argtypes = [vp, C.POINTER(Scene), C.POINTER(RtcCamera), C.POINTER(RtcRenderDesc), vp, vp,
                                         vp, vp]
     L.rtc_deinterleave_async.argtypes = [vp, ip, ip, ip, ip, vp, vp]
+    if hasattr(L, "rtc_deinterleave_bands_async"):  # (absent from round-4 libraries loaded for A/B timing)
+        L.rtc_deinterleave_bands_async.argtypes = [vp, ip, ip, ip, ip, ip, vp, vp]
     L.rtc_probe_ray_triangle.argtypes = [vp, vp, sz, vp, vp]
     L.rtc_probe_ray_sphere.argtypes = [vp, vp, sz, vp, vp, vp]
     L.rtc_probe_environment.argtypes = [vp, vp, sz, vp]

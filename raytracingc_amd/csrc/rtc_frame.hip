@@ -212,14 +212,47 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
                                const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int G,
                                Color *outImage, float *outAccum, RtcStats *stats, std::chrono::steady_clock::time_point t0);
 
+/* Part g of G of a full frame d: rows y = g + k*G, or the bands b = g, g + G, ... of d->rowBand rows (rtc.h) */
+static RtcRenderDesc part_desc(const RtcRenderDesc *d, int g, int G)
+{
+    RtcRenderDesc p = *d;
+    const int B = d->rowBand > 1 ? d->rowBand : 1;
+    p.rowStart = g * B;
+    p.rowStride = G;
+    p.rowBand = B;
+    return p;
+}
+
+/* A part's compact rows (d: its part_desc; `elem` bytes per pixel component -- 1 for Color, 4 for the float
+ * accumulator) into their places of a host frame of width d->width: one SDMA rectangle per band size (the full bands as
+ * rows of B image rows, pitch rowStride*B rows; then the last, partial band), rtc_copy_rows_d2h_dma */
+static int copy_part_to_host(unsigned char *hostFrame, const RtcRenderDesc *d, const void *devRows, size_t elem)
+{
+    const int rows = rtc_rows_selected(d);
+    const int B = d->rowBand > 1 ? d->rowBand : 1;
+    const size_t rowBytes = (size_t)d->width * 3 * elem;
+    unsigned char *dst = hostFrame + (size_t)d->rowStart * rowBytes;
+    const size_t hostPitch = (size_t)d->rowStride * B * rowBytes;
+    const int full = rows / B, tail = rows - full * B;
+    if (full > 0)
+        if (int rc = rtc_copy_rows_d2h_dma(dst, hostPitch, devRows, (size_t)B * rowBytes, (size_t)B * rowBytes, full))
+            return rc;
+    if (tail > 0)
+        return rtc_copy_rows_d2h_dma(dst + (size_t)full * hostPitch, rowBytes,
+                                     (const unsigned char *)devRows + (size_t)full * B * rowBytes, rowBytes, rowBytes,
+                                     tail);
+    return 0;
+}
+
 extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                                 const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
                                 Color *outImage, float *outAccum, RtcStats *stats)
 {
     const auto t0 = std::chrono::steady_clock::now();
     if (!scene || !cam || !d || !outImage || numDevices <= 0 || d->rowStart != 0 || d->rowStride != 1 ||
-        d->width <= 0 || d->height <= 0)
-        return rtc_fail(RTC_EINVAL, "rtc_render_multi: bad argument (full frames only)");
+        d->width <= 0 || d->height <= 0 || d->rowBand < 0 || d->rowBand > 64 || (d->rowBand & (d->rowBand - 1)) != 0)
+        return rtc_fail(RTC_EINVAL, "rtc_render_multi: bad argument (full frames only; rowBand: the bands the devices "
+                                    "interleave, 0/1 or a power of two <= 64)");
     int n = 0;
     if (int rc = rtc_device_count(&n))
         return rc;
@@ -233,7 +266,8 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         return rtc_fail(RTC_ENODEV, "rtc_render_multi: RCCL (librccl.so.1) could not be loaded: %s", dlerror());
     RtcDeviceGuard guard(-1);
     const int G = numDevices, W = d->width, H = d->height;
-    const int rowsPer = (H + G - 1) / G; /* every part padded to rank 0's row count for the gather */
+    const RtcRenderDesc d0 = part_desc(d, 0, G);
+    const int rowsPer = rtc_rows_selected(&d0); /* every part padded to part 0's row count (the largest) for the gather */
     const size_t partPx = (size_t)rowsPer * (size_t)W;
 
     /* one communicator per device (single-process clique) */
@@ -286,9 +320,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
         RtcDeviceGuard dg(g);
-        RtcRenderDesc dg_desc = *d;
-        dg_desc.rowStart = g;
-        dg_desc.rowStride = G;
+        const RtcRenderDesc dg_desc = part_desc(d, g, G);
         p.rows = rtc_rows_selected(&dg_desc);
         if (int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s))
             return rc;
@@ -324,9 +356,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
         RtcDeviceGuard dg(g);
-        RtcRenderDesc dg_desc = *d;
-        dg_desc.rowStart = g;
-        dg_desc.rowStride = G;
+        const RtcRenderDesc dg_desc = part_desc(d, g, G);
         HIP_TRY(hipEventRecord(p.e0, p.st));
         if (int rc = rtc_render_rows_async(p.s, scene, cam, &dg_desc, p.col.p, p.acc.p, p.seg.p, p.st))
             return rc;
@@ -347,7 +377,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     {
         RtcDeviceGuard dg(0);
         hipStream_t st0 = parts[0].st;
-        if (int rc = rtc_deinterleave_async(gathered.p, G, rowsPer, W, H, frame.p, st0))
+        if (int rc = rtc_deinterleave_bands_async(gathered.p, G, rowsPer, W, H, d0.rowBand, frame.p, st0))
             return rc;
         HIP_TRY(hipMemcpyAsync(hColors.p, frame.p, (size_t)W * H * 3, hipMemcpyDeviceToHost, st0));
         HIP_TRY(hipEventRecord(eFrame, st0));
@@ -358,7 +388,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     const double frameMs = ms_since(f0);
     if (outAccum) { /* a float row is 4x the bytes of a Color row: re-interleave it as 4W "pixels" */
         RtcDeviceGuard dg(0);
-        if (int rc = rtc_deinterleave_async(gatheredAcc.p, G, rowsPer, 4 * W, H, frameAcc.p, parts[0].st))
+        if (int rc = rtc_deinterleave_bands_async(gatheredAcc.p, G, rowsPer, 4 * W, H, d0.rowBand, frameAcc.p, parts[0].st))
             return rc;
     }
     double renderMs = 0.0;
@@ -393,7 +423,8 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
 {
     RtcDeviceGuard guard(-1);
     const int W = d->width, H = d->height;
-    const int rowsPer = (H + G - 1) / G;
+    const RtcRenderDesc d0 = part_desc(d, 0, G);
+    const int rowsPer = rtc_rows_selected(&d0);
     const size_t partPx = (size_t)rowsPer * (size_t)W;
     PinnedBuf hColors, hAccum; /* before the parts: destroyed after their streams are synchronised */
     HIP_TRY(hColors.alloc((size_t)W * H * 3));
@@ -427,9 +458,7 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
         RtcDeviceGuard dg(g);
-        RtcRenderDesc dg_desc = *d;
-        dg_desc.rowStart = g;
-        dg_desc.rowStride = G;
+        const RtcRenderDesc dg_desc = part_desc(d, g, G);
         p.rows = rtc_rows_selected(&dg_desc);
         if (int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s))
             return rc;
@@ -447,9 +476,7 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
     for (int g = 0; g < G; ++g) {
         Part &p = parts[g];
         RtcDeviceGuard dg(g);
-        RtcRenderDesc dg_desc = *d;
-        dg_desc.rowStart = g;
-        dg_desc.rowStride = G;
+        const RtcRenderDesc dg_desc = part_desc(d, g, G);
         HIP_TRY(hipEventRecord(p.e0, p.st));
         if (int rc = rtc_render_rows_async(p.s, scene, cam, &dg_desc, p.col.p, p.acc.p, p.seg.p, p.st))
             return rc;
@@ -465,8 +492,8 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
             if (e != hipSuccess) {
                 p.rc = rtc_fail(-(int)e, "rtc_render_multi: device %d: %s", g, hipGetErrorString(e));
             } else {
-                p.rc = rtc_copy_rows_d2h_dma((unsigned char *)hColors.p + (size_t)g * W * 3, (size_t)G * W * 3,
-                                             p.col.p, (size_t)W * 3, (size_t)W * 3, p.rows);
+                const RtcRenderDesc pd = part_desc(d, g, G);
+                p.rc = copy_part_to_host((unsigned char *)hColors.p, &pd, p.col.p, 1);
             }
             if (p.rc)
                 p.err = rtc_last_error();
@@ -489,11 +516,11 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
         HIP_TRY(hipMemcpy(sg, p.seg.p, kSegBytes, hipMemcpyDeviceToHost));
         for (int k = 0; k < RTC_SEGMENT_COUNTERS; ++k)
             seg[k] += sg[k];
-        if (outAccum)
-            if (int rc = rtc_copy_rows_d2h_dma((float *)hAccum.p + (size_t)g * W * 3, (size_t)G * W * 3 * sizeof(float),
-                                               p.acc.p, (size_t)W * 3 * sizeof(float), (size_t)W * 3 * sizeof(float),
-                                               p.rows))
+        if (outAccum) {
+            const RtcRenderDesc pd = part_desc(d, g, G);
+            if (int rc = copy_part_to_host((unsigned char *)hAccum.p, &pd, p.acc.p, sizeof(float)))
                 return rc;
+        }
     }
     memcpy(outImage, hColors.p, (size_t)W * H * 3);
     if (outAccum)
@@ -806,9 +833,9 @@ extern "C" int rtc_dma_debug_inflight(void *p, size_t bytes, int pending)
 /* ---- pipelined frames (the host frame loop) -------------------------------------------------------------------
  * A frame sequence on one device, driven from native code so the per-frame host cost is the launch enqueue alone:
  * frame k renders the rows of d (RTC_F_OVERLAP: its preparation overlaps frame k-1's sky pass) into devRows[k %
- * nbuf]; a copy thread waits for the frame's event and moves its rows into hostRows[k % nbuf] (row pitch hostPitch:
- * a rank's rows y = rowStart + j*rowStride land in the interleaved host frame when hostRows points at row rowStart
- * and hostPitch = rowStride * width * 3) on the SDMA engines; buffer b is rendered into again once its copy has
+ * nbuf]; a copy thread waits for the frame's event and moves its rows into hostRows[k % nbuf] (pitch hostPitch between
+ * consecutive rows -- or bands of d->rowBand rows: a rank's rows y = rowStart + j*rowStride land in the interleaved host
+ * frame when hostRows points at row rowStart and hostPitch = rowStride * rowBand * width * 3) on the SDMA engines; buffer b is rendered into again once its copy has
  * finished.  The reference's equivalent is main.c:285-305: the threads write their rows into the shared image, which
  * stbi_write_bmp then reads. */
 
@@ -823,8 +850,9 @@ extern "C" int rtc_frame_loop_cameras(RtcDeviceScene *s, const Scene *scene, con
             return rtc_fail(RTC_EINVAL, "rtc_frame_loop: null buffer %d", b);
     const int rows = rtc_rows_selected(d);
     const size_t rowBytes = (size_t)(d->width > 0 ? d->width : 0) * 3;
-    if (rows > 1 && hostPitch < rowBytes)
-        return rtc_fail(RTC_EINVAL, "rtc_frame_loop: host pitch %zu < row bytes %zu", hostPitch, rowBytes);
+    const int B = d->rowBand > 1 ? d->rowBand : 1;
+    if (rows > B && hostPitch < (size_t)B * rowBytes)
+        return rtc_fail(RTC_EINVAL, "rtc_frame_loop: host pitch %zu < band bytes %zu", hostPitch, (size_t)B * rowBytes);
     int device = 0;
     HIP_TRY(hipGetDevice(&device));
     RtcRenderDesc dd = *d;
@@ -863,7 +891,15 @@ extern "C" int rtc_frame_loop_cameras(RtcDeviceScene *s, const Scene *scene, con
                 rc = rtc_fail(-(int)e, "rtc_frame_loop: frame event: %s", hipGetErrorString(e));
             } else {
                 const auto c0 = std::chrono::steady_clock::now();
-                rc = rtc_copy_rows_d2h_dma(hostRows[b], hostPitch, devRows[b], rowBytes, rowBytes, rows);
+                /* bands of B rows (d->rowBand): the full bands as rows of B image rows at the band pitch, then the
+                 * last, partial band (single rows: B = 1, one rectangle) */
+                const int full = rows / B, tail = rows - full * B;
+                rc = full > 0 ? rtc_copy_rows_d2h_dma(hostRows[b], hostPitch, devRows[b], B * rowBytes, B * rowBytes, full)
+                              : 0;
+                if (!rc && tail > 0)
+                    rc = rtc_copy_rows_d2h_dma((unsigned char *)hostRows[b] + (size_t)full * hostPitch, rowBytes,
+                                               (const unsigned char *)devRows[b] + (size_t)full * B * rowBytes, rowBytes,
+                                               rowBytes, tail);
                 ms = ms_since(c0);
             }
             std::lock_guard<std::mutex> lk(m);

@@ -39,6 +39,7 @@ static_assert(sizeof(Triangle) == 68, "Triangle layout");
 static_assert(sizeof(Scene) == 56, "Scene layout");
 static_assert(sizeof(Color) == 3, "Color layout");
 static_assert(sizeof(Ray) == 24, "Ray layout");
+static_assert(sizeof(RtcRenderDesc) == 36, "RtcRenderDesc layout (ctypes mirror: raytracingc_amd/_abi.py)");
 
 using namespace rtcdev;
 
@@ -162,7 +163,7 @@ static_assert(kGeoSetInts >= kGeoLists * kGeoCountStride, "a counter set holds e
 struct SkyKey {
     const void *colors, *accum;
     float cam[13], env[14];
-    int dims[8];
+    int dims[9];
 };
 struct RtcDeviceScene {
     int device;
@@ -615,9 +616,12 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
 
 extern "C" int rtc_rows_selected(const RtcRenderDesc *d)
 {
-    if (!d || d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height || d->height <= 0)
+    if (!d || d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height || d->height <= 0 || d->rowBand < 0)
         return 0;
-    return (d->height - d->rowStart + d->rowStride - 1) / d->rowStride;
+    /* bands of B rows (rowBand, rtc.h): the full bands' rows, plus the last band's rows inside the frame */
+    const long long B = d->rowBand > 1 ? d->rowBand : 1, step = (long long)d->rowStride * B;
+    const long long nb = (d->height - d->rowStart + step - 1) / step, last = d->rowStart + (nb - 1) * step;
+    return (int)((nb - 1) * B + std::min<long long>(B, d->height - last));
 }
 
 /* ---- the render kernel ---------------------------------------------------------------------------- */
@@ -664,6 +668,7 @@ struct RenderParams {
     unsigned long long *__restrict__ segSlots; /* kSegSlots x kSegSlotStride partial counters (flush_counters) */
     int triCount, triPadded, sphereCount, maskWords;
     int width, height, rows, rowStart, rowStride;
+    int rowBandShift; /* log2 of the rows per band (rtc.h rowBand): 0 = single rows */
     int spp, maxBounce;
     int hoist;
     float invSpp; /* (float)(1. / accumulationCount), main.c:99 */
@@ -702,6 +707,51 @@ template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
 #define KLOAD(p, i) ((p)[i])
 #endif
 
+/* A RenderParams field of the launch, re-read from the kernarg segment where it is used (RTC_KARG; values, and pointers
+ * read through KCONST / KLOAD / gload only -- a pointer loaded this way has no known address space, so a plain vector
+ * access through it would be a flat one, whose wait covers lgkmcnt too): the kernel's one
+ * argument is RenderParams at offset 0 of that segment.  The segment pointer is laundered through an empty asm at every
+ * use, so the scalar load is neither hoisted out of the loops nor merged with another use: the field occupies no SGPR
+ * between uses.  rtc_render_chain keeps ~60 SGPRs of launch constants (camera, environment, dimensions, pointers)
+ * otherwise, and spilled 155 SGPRs to VGPR lanes (v_writelane / v_readlane in its loops).  For fields
+ * read once per item, window or escaped bounce: a scalar-cache hit against a register that would have been spilled. */
+#ifndef RTC_KARG
+#define RTC_KARG 1
+#endif
+/* 0 in a vector register the compiler cannot see through: a wave-uniform address plus vzero() is read by a vector load
+ * (waited for by vmcnt, in order) instead of a scalar load */
+__device__ __forceinline__ int vzero()
+{
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+/* a dword of global memory by a global (not flat) vector load: a flat load's wait would also cover the LDS and scalar
+ * loads (lgkmcnt) */
+template <typename T> __device__ __forceinline__ unsigned gload(const T *p, size_t i)
+{
+    static_assert(sizeof(T) == 4, "dwords");
+    return ((const __attribute__((address_space(1))) unsigned *)p)[i];
+}
+template <typename T> __device__ __forceinline__ T karg_at(size_t off)
+{
+    const __attribute__((address_space(4))) char *base =
+        (const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(base));
+    static_assert(sizeof(T) % 4 == 0, "dword fields");
+    T v;
+    const __attribute__((address_space(4))) unsigned *q = (const __attribute__((address_space(4))) unsigned *)(base + off);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k)
+        ((unsigned *)&v)[k] = q[k];
+    return v;
+}
+#if RTC_KARG
+#define KARG(field) karg_at<decltype(RenderParams::field)>(offsetof(RenderParams, field))
+#else
+#define KARG(field) (P.field)
+#endif
+
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 
 
@@ -721,6 +771,14 @@ __device__ __forceinline__ V3 primary_dir(const RenderParams &P, int x, int y)
     return normalized(add(add(mul(P.ex, dx), mul(P.ey, dy)), mul(P.ez, P.fov)));
 }
 
+/* Launch row r -> image row y: y = rowStart + k*rowStride (main.c:84's interleave), or bands of 2^rowBandShift rows
+ * (rtc.h rowBand): y = rowStart + (r / B)*rowStride*B + r % B */
+__device__ __forceinline__ int launch_row_y(const RenderParams &P, int r)
+{
+    const int sh = P.rowBandShift;
+    return P.rowStart + ((r >> sh) * P.rowStride << sh) + (r & ((1 << sh) - 1));
+}
+
 __device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P, int bx, int by)
 {
     PixelRay px;
@@ -729,7 +787,7 @@ __device__ __forceinline__ PixelRay pixel_ray(const RenderParams &P, int bx, int
     px.x = bx * kTileW + (wave & 1) * 8 + (lane & 7);
     px.r = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
     px.valid = px.x < P.width && px.r < P.rows;
-    px.y = P.rowStart + px.r * P.rowStride;
+    px.y = launch_row_y(P, px.r);
     px.dir = primary_dir(P, px.x, px.y);
     return px;
 }
@@ -1121,7 +1179,8 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
 }
 /* heavy-kernel section cycles (s_memtime deltas summed over waves): 0 primary trace, 1 cluster tests,
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
-__device__ unsigned long long g_rtc_sect[16]; /* [8..] window statistics (rtc_render_chain) */
+constexpr int kDiagSects = 24;
+__device__ unsigned long long g_rtc_sect[kDiagSects]; /* [8..12] window statistics (rtc_render_chain) */
 #define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 /* per-block records of rtc_tile_cull (wave 0): {start, level 1 done, end, geometry, level-2 prefilter cycles, candidate
  * loop cycles, candidates, 0}, written with plain stores into the buffer rtc_diag_set_cull_buffer names (null: none) */
@@ -1138,7 +1197,7 @@ extern "C" int rtc_diag_set_cull_buffer(void *dptr)
             r_[0] = (a), r_[1] = (b), r_[2] = (c), r_[3] = (geo), r_[4] = (pre), r_[5] = (loop), r_[6] = (cand); \
         }                                                                                                      \
     } while (0)
-__shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..15 (rtc_render_chain) */
+__shared__ unsigned long long s_rtc_sect[4][kDiagSects]; /* [wave][section]: 0..7, 13..23 (rtc_render_chain) */
 #define DSECT_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define DSECT_END(v, k)                                                                                        \
     do {                                                                                                       \
@@ -1146,12 +1205,24 @@ __shared__ unsigned long long s_rtc_sect[16][16]; /* [wave][section]: 0..7, 13..
         if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))                           \
             s_rtc_sect[threadIdx.x >> 6][k] += dsectNow - (v);                                                 \
     } while (0)
-extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
+/* Uniform section marks: the cycles since the previous mark of the wave go to section k.  Placed at wave-uniform points
+ * only, the marks tile the loop: every cycle between the kernel's first mark and its last lands in exactly one section
+ * (the BEGIN/END pairs above nest inside them) */
+#define DMARK_INIT(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DMARK(v, k)                                                                                            \
+    do {                                                                                                       \
+        const unsigned long long dmarkNow = __builtin_amdgcn_s_memtime();                                      \
+        if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))                           \
+            s_rtc_sect[threadIdx.x >> 6][k] += dmarkNow - (v);                                                 \
+        (v) = dmarkNow;                                                                                        \
+    } while (0)
+extern "C" int rtc_diag_sections(unsigned long long *out, int reset)
 {
-    if (out8)
-        HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_rtc_sect), 16 * sizeof(unsigned long long)));
+    /* out: kDiagSects (24) counters */
+    if (out)
+        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_sect), kDiagSects * sizeof(unsigned long long)));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[kDiagSects] = {0};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
     }
     return 0;
@@ -1159,6 +1230,8 @@ extern "C" int rtc_diag_sections(unsigned long long *out8, int reset)
 #else
 #define DSECT_BEGIN(v) (void)0
 #define DSECT_END(v, k) (void)0
+#define DMARK_INIT(v) (void)0
+#define DMARK(v, k) (void)0
 #define CSTAMP(v) (void)0
 #define CREC(blk, a, b, c, geo, pre, loop, cand) (void)0
 #endif
@@ -1197,7 +1270,7 @@ __device__ TileCone rect_cone(const RenderParams &P, int x0, int x1, int r0, int
     TileCone K;
     x1 = min(x1, P.width - 1);
     r1 = min(r1, P.rows - 1);
-    const int y0 = P.rowStart + r0 * P.rowStride, y1 = P.rowStart + r1 * P.rowStride;
+    const int y0 = launch_row_y(P, r0), y1 = launch_row_y(P, r1); /* (y is increasing in the launch row) */
     /* the same f32 expressions as primary_dir */
     const float dxs[2] = {(float)(x0 - P.width / 2) / (float)(P.height / 2),
                           (float)(x1 - P.width / 2) / (float)(P.height / 2)};
@@ -1813,7 +1886,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
         px.x = bx * kTileW + (w16 & 1) * 8 + (lane & 7);
         px.r = by * kTileH + (w16 >> 1) * 8 + (lane >> 3);
         px.valid = px.x < P.width && px.r < P.rows;
-        px.y = P.rowStart + px.r * P.rowStride;
+        px.y = launch_row_y(P, px.r);
         px.dir = primary_dir(P, px.x, px.y);
         px.valid = px.valid && !((geo >> lane) & 1ull);
         V3 acc{0.f, 0.f, 0.f};
@@ -1971,6 +2044,7 @@ struct ChainWaveLds {
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
 static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
 static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
+static_assert(RTC_CHAIN_PAIRS * sizeof(unsigned short) >= 3 * 64 * sizeof(float), "a window's staged samples fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
 constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
@@ -1988,7 +2062,10 @@ constexpr size_t chain_lds_floor(int n) { return n >= 4 ? 0 : kCuLds / (size_t)(
 /* The clustered records staged in LDS structure-of-arrays: 16-B quarter k of record i at q[k * n + i], n = the
  * staged record count.  Lanes reading different records then hit different banks in ds_read_b128's 16-lane
  * groups (64-B records at lane-varying indices put four lanes of a group on each bank); one record is still four
- * ds_read_b128. */
+ * ds_read_b128.  (Round 5 tried a slot skipped after every cluster, for pair passes whose lanes read record j of
+ * different clusters: conflict cycles 3.8 M -> 5.0 M per 1080p launch -- the pair list is cluster-major, so a pass's
+ * lanes mostly share a cluster, while the reach table's consecutive records then straddled the skipped slots.) */
+__host__ __device__ constexpr int soa_slots(int n) { return n; }
 __device__ __forceinline__ DevTri rec_soa(const float4 *__restrict__ q, int n, int i)
 {
     DevTri t;
@@ -2124,7 +2201,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         if (r8l) {
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(live >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)live, 0u));
-            const ClusterTerms t = cluster_terms(p0, P.clusters[lane]);
+            /* (the workgroup's LDS copy of the clusters: a global load here was a round trip on every window) */
+            const ClusterTerms t = cluster_terms(p0, RTC_DENSE_CULL ? sCl[lane] : P.clusters[lane]);
             W.cl[pos][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
             W.cl[pos][1] = make_float4(t.A, t.B, __int_as_float(lane), __int_as_float((int)r8l));
         }
@@ -2309,21 +2387,25 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 /* Primary segments over the tile's candidates (rtc_render_chain) with the filter records staged in LDS (null: from
  * global memory): the filter's record is an LDS read instead of a dependent scalar load per candidate; DevPrimX
  * (survivors only) stays global.  Same operations as closest_primary_listed. */
-__device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P, V3 dir, Closest &c,
-                                                           const unsigned long long *__restrict__ mask,
+__device__ __forceinline__ void closest_primary_listed_lds(V3 dir, Closest &c, const unsigned long long *__restrict__ mask,
+                                                           unsigned long long m0, unsigned long long m1,
                                                            const DevPrimF *__restrict__ sF, bool staged)
 {
-    for (int w = 0; w < P.maskWords; ++w) {
-        unsigned long long m = KCONST(mask)[w];
+    /* m0, m1: the tile's first two mask words, already read (the chain kernel prefetches them one item ahead) */
+    const int maskWords = KARG(maskWords);
+    const DevPrimF *const primF = KARG(primF);
+    const DevPrimX *const primX = KARG(primX);
+    for (int w = 0; w < maskWords; ++w) {
+        unsigned long long m = w == 0 ? m0 : w == 1 ? m1 : KCONST(mask)[w];
         while (m) {
             const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
             /* two loads of known address space (LDS, or a scalar load): a pointer that may be either would be
              * read with flat loads, whose wait also covers the wave's pending slot stores */
-            const DevPrimF F = staged ? sF[t] : KLOAD(P.primF, t);
+            const DevPrimF F = staged ? sF[t] : KLOAD(primF, t);
             if (!prim_backfacing(dir, F) && prim_pass(dir, F) && !(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
                 /* the reference's arithmetic (raytracing.c:189-208) */
-                const DevPrimX X = KLOAD(P.primX, t);
+                const DevPrimX X = KLOAD(primX, t);
                 const V3 h = cross(dir, V3{X.acx, X.acy, X.acz});
                 const float det = dot(V3{X.abx, X.aby, X.abz}, h);
                 if (!(-kEps < det && det < kEps)) {
@@ -2355,12 +2437,12 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
     if (!MULTI)
         S.rec = (float4 *)sDyn;
     if (P.chainPrimF)
-        S.primF = (DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
-    const int nRec = P.clusterCount * kClusterSize;
+        S.primF = (DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)soa_slots(P.clusterCount * kClusterSize) * sizeof(DevTri)));
+    const int nRec = P.clusterCount * kClusterSize, slots = soa_slots(nRec);
     for (int i = threadIdx.x; S.rec && i < nRec; i += kChainBlock) {
         const float4 *g = (const float4 *)(P.clTris + i);
         for (int k = 0; k < 4; ++k)
-            S.rec[k * nRec + i] = g[k];
+            S.rec[k * slots + i] = g[k];
     }
     for (int i = threadIdx.x; S.primF && i < P.triPadded; i += kChainBlock)
         S.primF[i] = P.primF[i];
@@ -2372,6 +2454,8 @@ template <bool MULTI, bool COUNT> /* MULTI: more than one chunk of clusters (chu
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
+    DSECT_BEGIN(dtot);
+    DMARK_INIT(dcur);
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
@@ -2389,13 +2473,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
     const float4 *sRec = S.rec;
     /* the staged primary filter records: always the LDS address (never null), used when P.chainPrimF */
-    const DevPrimF *sPF = (const DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)P.clusterCount * kClusterSize * sizeof(DevTri)));
+    const DevPrimF *sPF = (const DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)soa_slots(P.clusterCount * kClusterSize) * sizeof(DevTri)));
     const bool pfStaged = P.chainPrimF != 0;
 #ifdef RTC_DIAG
-    if ((threadIdx.x & 63) < 16)
+    if ((threadIdx.x & 63) < kDiagSects)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+    static_assert(kChainBlock / 64 <= 4, "s_rtc_sect holds four waves");
 #endif
-    DSECT_BEGIN(dtot);
     __syncthreads();
     sPow.attach(P.env);
     const int lane = threadIdx.x & 63;
@@ -2411,7 +2495,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #define RTC_NEXT_ITEM() ((int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x)
     if (lane == 0)
         nextIt = RTC_NEXT_ITEM();
-    const int tilesX = P.blocksX * 2;
+    /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
+     * segment where they are used: KARG) */
     constexpr bool counting = COUNT;
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0, segSpec = 0;
@@ -2428,36 +2513,86 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             incl += v;
     }
     const int nItems = __builtin_amdgcn_readlane(incl, kGeoLists - 1);
+    /* Prefetch (round 5): an item's list entry and its tile's first two mask words were written by the tile cull on
+     * other XCDs, so their first reads miss this XCD's L2; read as scalar loads at the item's start they were a chain
+     * of dependent misses on the critical path of every item (round-4 stamps: item setup 17 % of the waves' lifetime).
+     * Here they are VECTOR loads issued one item ahead: the next item's entry at this item's start, its tile's mask
+     * dwords (lane j < 4: dword j) at this item's first bounce iteration, once the entry is back.  Vector loads return in
+     * order and are waited for by vmcnt, so a scalar wait never completes them early.  Each lives in one register that
+     * is consumed before it is reloaded (a loop-carried copy of an in-flight load would wait for it at the copy), and
+     * neither is in flight at a loop preheader that flushes vmcnt (after the bounce loop, the walk's did). */
+#ifndef RTC_ITEM_PREFETCH
+#define RTC_ITEM_PREFETCH 1
+#endif
+    const auto entry_of = [&](int it2) -> size_t {
+        const int l = (int)__popcll(__ballot(lane < kGeoLists && incl <= it2));
+        const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
+        return (size_t)l * KARG(geoCap) + (size_t)(it2 - base);
+    };
+    const auto mask_dwords = [&](int code2) -> unsigned {
+        const unsigned *mw = (const unsigned *)(KARG(tileMask) + (size_t)(code2 >> 6) * P.maskWords);
+        return lane < 2 * P.maskWords && lane < 4 ? gload(mw, (size_t)lane) : 0u;
+    };
+    int it = __builtin_amdgcn_readfirstlane(nextIt);
+    unsigned vc = 0, vm = 0; /* the current item's entry and mask dwords (vector registers) */
+    if (RTC_ITEM_PREFETCH && it < nItems) {
+        vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
+        vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+    }
+    if (lane == 0)
+        nextIt = RTC_NEXT_ITEM();
+    DMARK(dcur, 19); /* prologue: staging, tables, the first item */
     for (;;) {
-        DSECT_BEGIN(dset);
-        const int it = __builtin_amdgcn_readfirstlane(nextIt);
         if (it >= nItems)
             break;
-        const int l = (int)__popcll(__ballot(lane < kGeoLists && incl <= it));
-        const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
+#if RTC_ITEM_PREFETCH
+        const int code = __builtin_amdgcn_readfirstlane((int)vc);
+        const unsigned long long m0 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 0) |
+                                      (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 1) << 32;
+        const unsigned long long m1 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 2) |
+                                      (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 3) << 32;
+#else /* round 4: scalar loads at the item's start */
+        const int code = __builtin_amdgcn_readfirstlane(KCONST(KARG(geoList))[entry_of(it)]);
+        const unsigned long long *mk = KARG(tileMask) + (size_t)(code >> 6) * P.maskWords;
+        const unsigned long long m0 = KCONST(mk)[0], m1 = P.maskWords > 1 ? KCONST(mk)[1] : 0ull;
+#endif
+        /* the next item: its number (the LDS counter read at this item's previous start), its entry, and the counter for
+         * the one after */
+        const int itNext = __builtin_amdgcn_readfirstlane(nextIt);
+        if (RTC_ITEM_PREFETCH && itNext < nItems)
+            vc = gload(KARG(geoList), entry_of(itNext) + (size_t)vzero());
+        /* the next item's mask dwords requested (none needed past the end) */
+        bool maskNext = !RTC_ITEM_PREFETCH || itNext >= nItems;
         if (lane == 0)
             nextIt = RTC_NEXT_ITEM();
-        const int code = __builtin_amdgcn_readfirstlane(KCONST(P.geoList)[(size_t)l * P.geoCap + (it - base)]);
         const int tile = code >> 6, bit = code & 63;
+        const int tilesX = KARG(blocksX) * 2;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
-        const int y = P.rowStart + r * P.rowStride;
-        const V3 pdir = primary_dir(P, x, y); /* main.c:88-94 */
-        const unsigned long long *mask = P.tileMask + (size_t)tile * P.maskWords;
+        const int sh = KARG(rowBandShift); /* launch_row_y */
+        const int y = KARG(rowStart) + ((r >> sh) * KARG(rowStride) << sh) + (r & ((1 << sh) - 1));
+        V3 pdir; /* main.c:88-94, as primary_dir */
+        {
+            const int W = KARG(width), H = KARG(height);
+            const float dx = (float)(x - W / 2) / (float)(H / 2);
+            const float dy = (float)(y - H / 2) / (float)(H / 2);
+            pdir = normalized(add(add(mul(KARG(ex), dx), mul(KARG(ey), dy)), mul(KARG(ez), KARG(fov))));
+        }
+        const unsigned long long *mask = KARG(tileMask) + (size_t)tile * P.maskWords;
         unsigned L = 0;
         if (counting)
             for (int w = 0; w < P.maskWords; ++w)
                 L += (unsigned)__popcll(mask[w]);
-        const unsigned seed = (unsigned)(x + y * P.width); /* main.c:95 */
+        const unsigned seed = (unsigned)(x + y * KARG(width)); /* main.c:95 */
         const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            closest_primary_listed_lds(P, pdir, prim, mask, sPF, pfStaged);
+            closest_primary_listed_lds(pdir, prim, mask, m0, m1, sPF, pfStaged);
             if (counting && lane == 0) {
                 segTraced++;
                 segTests += L;
             }
         }
-        DSECT_END(dset, 15);
+        DMARK(dcur, 15); /* item setup */
         /* in-kernel sums (items without a deferred slot): the pixel's accumulator (main.c:97), component c in lane c */
         float acc = 0.f;
         int k = 0;       /* samples accumulated */
@@ -2469,14 +2604,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             const int est = k > 0 ? (int)(((unsigned long long)need * jn + (unsigned)k - 1u) / (unsigned)k) : need;
             const int nAct = min(64, est + (est >> 3) + 1);
             const bool act = lane < nAct;
-            DSECT_BEGIN(dc0);
             /* the lane's start state: the seed advanced by 7 (jn + lane) draws = the wave-uniform state at jn,
              * then this lane's fixed jump by 7 lane draws (both affine LCG compositions, rng_advance) */
             const unsigned s0 = (unsigned)__builtin_amdgcn_readfirstlane((int)rng_advance(seed, 7u * jn));
             unsigned rng = s0 * laneJump.a + laneJump.c;
-            DSECT_END(dc0, 0);
+            DMARK(dcur, 0); /* window setup */
             /* ---- S_{jn + lane}: one calcColor (raytracing.c:262-296) ---- */
-            V3 pos = P.origin, dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
+            V3 pos = KARG(origin), dir = pdir, rayColor{1.f, 1.f, 1.f}, light{0.f, 0.f, 0.f};
             int bounce = 0;
             unsigned hits = 0, calls = 0, tests = 0, clTests = 0;
             bool alive = act;
@@ -2488,24 +2622,28 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
-                    DSECT_BEGIN(dc1);
                     if (alive) {
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            closest_primary_listed_lds(P, dir, c, mask, sPF, pfStaged);
+                            closest_primary_listed_lds(dir, c, mask, m0, m1, sPF, pfStaged);
                             if (counting)
                                 tests += L;
                         }
                     }
-                    DSECT_END(dc1, 1);
+                    DMARK(dcur, 1); /* primary trace */
                 } else { /* bounce segments of the live lanes (the whole wave takes part) */
+                    if (!maskNext) { /* the next item's mask dwords (see the prefetch above) */
+                        vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+                        maskNext = true;
+                    }
                     unsigned t = 0;
                     c = chain_trace_pairs<MULTI, COUNT>(P, alive, bounce1, pos, dir, sRec, W, lane, t, sCl);
                     if (counting && alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
                     }
+                    DMARK(dcur, 17); /* bounce trace (14 table, 3 cull, 4 pair build, 5 pair passes inside) */
                 }
 #if RTC_DRAW_TABLE
                 /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
@@ -2526,10 +2664,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         DevMat M;
                         if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
                             const int u = __builtin_amdgcn_readfirstlane(c.idx);
-                            T = KLOAD(P.tris, u);
-                            M = KLOAD(P.mats, u);
+                            T = KLOAD(KARG(tris), u);
+                            M = KLOAD(KARG(mats), u);
                         } else {
-                            T = P.tris[c.idx];
+                            T = P.tris[c.idx]; /* (kernel-argument pointers: global loads, not flat) */
                             M = P.mats[c.idx];
                         }
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
@@ -2574,7 +2712,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #ifdef RTC_AB_CHEAP_ENV_CHAIN /* timing experiment only (the environment's cost in the chain kernel) */
                         light = add(light, mulv(lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y, 0.f)), rayColor));
 #else
-                        light = add(light, mulv(environment(dir, P.env), rayColor)); /* raytracing.c:291 */
+                        EnvParams env = KARG(env); /* the launch's sky and sun, the powf tables in LDS */
+                        sPow.attach(env);
+                        light = add(light, mulv(environment(dir, env), rayColor)); /* raytracing.c:291 */
 #endif
                         endSample = true;
                         DSECT_END(dc6, 6);
@@ -2582,26 +2722,29 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     if (endSample)
                         alive = false;
                 }
+                DMARK(dcur, 16); /* shading (2 hit, 6 environment inside) */
             }
             (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
-            DSECT_BEGIN(dc7);
-            const V3 t = mul(light, P.invSpp); /* calcColor(...) * (float)(1./spp), main.c:99 */
+            const V3 t = mul(light, KARG(invSpp)); /* calcColor(...) * (float)(1./spp), main.c:99 */
             const unsigned long long ones = __ballot(act && hits == 1u);
             unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
             int p = 0;
             SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
             /* in-kernel sums: the window's samples are staged in sample order in LDS -- the pair list's space, free
-             * until the next window's bounces; component c at stage[64 c + i] -- and lane c then adds them in order */
+             * until the next window's bounces; component c of staged sample i at stage[3 i + c] -- and lane c then adds
+             * them in order.  Interleaved, the three summing lanes read three consecutive dwords (three banks) and the
+             * staging lanes write at a stride of 3 dwords (a permutation of the 64 banks): no bank conflicts (round 4's
+             * stage[64 c + i] put the three readers on one bank: 6.3 M conflict cycles per 1080p launch) */
             float *const stage = (float *)W.pair;
             int staged = 0;
             auto flush = [&]() {
                 wave_lds_sync();
                 if (lane < 3) {
-                    const float *src = stage + 64 * lane;
+                    const float *src = stage + lane;
 #pragma unroll 8
                     for (int i = 0; i < staged; ++i)
-                        acc = acc + src[i];
+                        acc = acc + src[3 * i];
                 }
                 wave_lds_sync();
                 staged = 0;
@@ -2619,10 +2762,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
                 } else {
                     if (lane >= p && lane < p + take) {
-                        const int i = staged + lane - p;
+                        const int i = 3 * (staged + lane - p);
                         stage[i] = t.x;
-                        stage[64 + i] = t.y;
-                        stage[128 + i] = t.z;
+                        stage[i + 1] = t.y;
+                        stage[i + 2] = t.z;
                     }
                     staged += take;
                 }
@@ -2642,9 +2785,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         slot[kk] = SampleSlot{qx, qy, qz};
                 } else if (m == 1) {
                     if (lane == q) {
-                        stage[staged] = t.x;
-                        stage[64 + staged] = t.y;
-                        stage[128 + staged] = t.z;
+                        stage[3 * staged] = t.x;
+                        stage[3 * staged + 1] = t.y;
+                        stage[3 * staged + 2] = t.z;
                     }
                     ++staged;
                 } else { /* the staged samples first, then this one m times */
@@ -2676,21 +2819,26 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 if (act && mult == 0)
                     segSpec += tests;
             }
-            DSECT_END(dc7, 7);
+            DMARK(dcur, 7); /* walk and sums */
         }
         if (deferred) {
             if (lane == 0)
-                P.itemPix[it] = r * P.width + x;
+                P.itemPix[it] = r * KARG(width) + x;
         } else if (lane < 3) {
-            const size_t o = 3 * ((size_t)r * (size_t)P.width + (size_t)x) + (size_t)lane;
+            const size_t o = 3 * ((size_t)r * (size_t)KARG(width) + (size_t)x) + (size_t)lane;
             P.colors[o] = float_to_u8(acc);
             if (P.accum)
                 P.accum[o] = acc;
         }
+        if (!maskNext) /* (an item without a bounce iteration) */
+            vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+        it = itNext;
+        DMARK(dcur, 18); /* item tail: the pixel's colour */
     }
+    DMARK(dcur, 15);
 #ifdef RTC_DIAG
     DSECT_END(dtot, 13);
-    if (lane < 8 || (lane >= 13 && lane < 16))
+    if (lane < 8 || (lane >= 13 && lane < kDiagSects))
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
     /* [8] bounce-loop iterations, [9] live lanes summed over them, [10] window lanes, [11] windows, [12] lanes
      * whose sample was used */
@@ -2740,7 +2888,7 @@ static SkyKey sky_key(const RenderParams &P)
     k.cam[12] = P.fov;
     k.env[12] = P.env.focus;
     k.env[13] = P.env.intensity;
-    const int dims[8] = {P.width, P.height, P.rows, P.rowStart, P.rowStride, P.spp, P.maxBounce, P.hoist};
+    const int dims[9] = {P.width, P.height, P.rows, P.rowStart, P.rowStride, P.spp, P.maxBounce, P.hoist, P.rowBandShift};
     memcpy(k.dims, dims, sizeof dims);
     return k;
 }
@@ -2789,7 +2937,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     ms->frameEvent = nullptr;
     if (!scene || !cam || !d || !dColors)
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: null argument");
-    if (d->width <= 0 || d->height <= 0 || d->rowStride <= 0 || d->rowStart < 0)
+    if (d->width <= 0 || d->height <= 0 || d->rowStride <= 0 || d->rowStart < 0 || d->rowBand < 0 || d->rowBand > 64 ||
+        (d->rowBand & (d->rowBand - 1)) != 0)
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: bad geometry %dx%d rows %d+k*%d", d->width, d->height,
                         d->rowStart, d->rowStride);
     if ((long long)d->width * d->height > (1ll << 31) / 4)
@@ -2832,6 +2981,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.rows = rows;
     P.rowStart = d->rowStart;
     P.rowStride = d->rowStride;
+    P.rowBandShift = d->rowBand > 1 ? __builtin_ctz((unsigned)d->rowBand) : 0;
     P.spp = d->spp;
     P.maxBounce = d->maxBounce;
     P.hoist = (d->flags & RTC_F_HOIST_PRIMARY) ? 1 : 0;
@@ -3088,7 +3238,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
              * filter records when the block stays within 4 per CU */
             const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : RTC_CHAIN_WGS_FULL;
-            const size_t rec = s->chunkCount <= 1 ? (size_t)s->clusterCount * kClusterSize * sizeof(DevTri) : 0;
+            const size_t rec = s->chunkCount <= 1 ? (size_t)soa_slots(s->clusterCount * kClusterSize) * sizeof(DevTri) : 0;
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
             P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;
             const size_t floorLds = chain_lds_floor(wgsPerCu);
@@ -3156,18 +3306,41 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
 
 /* ---- row de-interleave after a gather (bytes) ----------------------------------------------------- */
 __global__ __launch_bounds__(256) void rtc_deinterleave_kernel(const unsigned char *__restrict__ in, int parts,
-                                                                int rowsPerPart, int rowBytes, int height,
+                                                                int rowsPerPart, int rowBytes, int height, int bandShift,
                                                                 unsigned char *__restrict__ out)
 {
-    /* one block-row per output row; 16-B vectors when the row is 16-B aligned */
+    /* one block-row per output row y: band b = y / B of part b % parts, the part's band b / parts */
     const int y = blockIdx.y;
     if (y >= height)
         return;
-    const int g = y % parts, k = y / parts;
+    const int b = y >> bandShift, j = y & ((1 << bandShift) - 1);
+    const int g = b % parts, k = ((b / parts) << bandShift) + j;
     const unsigned char *src = in + ((size_t)g * rowsPerPart + k) * (size_t)rowBytes;
     unsigned char *dst = out + (size_t)y * rowBytes;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rowBytes; i += gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+extern "C" int rtc_deinterleave_bands_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,
+                                            int rowBand, void *dOut, void *stream)
+{
+    if (!dCompact || !dOut || parts <= 0 || width <= 0 || height <= 0 || rowBand < 0 || rowBand > 64 ||
+        (rowBand & (rowBand - 1)) != 0)
+        return rtc_fail(RTC_EINVAL, "rtc_deinterleave_bands_async: bad argument");
+    const int B = rowBand > 1 ? rowBand : 1;
+    /* every part holds its bands' rows: part 0's count is the largest */
+    RtcRenderDesc d0{};
+    d0.width = width, d0.height = height, d0.rowStart = 0, d0.rowStride = parts, d0.rowBand = B;
+    if (rowsPerPart < rtc_rows_selected(&d0))
+        return rtc_fail(RTC_EINVAL, "rtc_deinterleave_bands_async: %d rows per part, part 0 has %d", rowsPerPart,
+                        rtc_rows_selected(&d0));
+    const int rowBytes = width * 3;
+    dim3 grid((rowBytes + 255) / 256 < 8 ? (rowBytes + 255) / 256 : 8, height);
+    hipLaunchKernelGGL(rtc_deinterleave_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char *)dCompact, parts, rowsPerPart, rowBytes, height, __builtin_ctz((unsigned)B),
+                       (unsigned char *)dOut);
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 extern "C" int rtc_deinterleave_async(const void *dCompact, int parts, int rowsPerPart, int width, int height,
@@ -3175,12 +3348,7 @@ extern "C" int rtc_deinterleave_async(const void *dCompact, int parts, int rowsP
 {
     if (!dCompact || !dOut || parts <= 0 || width <= 0 || height <= 0 || rowsPerPart * parts < height)
         return rtc_fail(RTC_EINVAL, "rtc_deinterleave_async: bad argument");
-    const int rowBytes = width * 3;
-    dim3 grid((rowBytes + 255) / 256 < 8 ? (rowBytes + 255) / 256 : 8, height);
-    hipLaunchKernelGGL(rtc_deinterleave_kernel, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const unsigned char *)dCompact, parts, rowsPerPart, rowBytes, height, (unsigned char *)dOut);
-    HIP_TRY(hipGetLastError());
-    return 0;
+    return rtc_deinterleave_bands_async(dCompact, parts, rowsPerPart, width, height, 1, dOut, stream);
 }
 
 /* A frame copy with a small footprint (rtc_copy_async): `blocks` workgroups stream 16-byte words (the byte tail

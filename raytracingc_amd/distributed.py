@@ -3,8 +3,9 @@ every GPU's own link (SharedHostFrames + rtc_frame_loop / rtc_copy_rows_d2h_dma)
 with RCCL over xGMI (FrameRenderer).
 
 The reference's only parallelism is the row interleave of its 12 pthreads (main.c:84: thread t renders rows
-y = t, t+12, ...).  Here rank r of G renders rows y = r + k*G into a compact [ceil(H/G), W, 3] uint8 buffer on
-its own GPU (the kernel seeds each pixel with its absolute index x + y*W, main.c:95, so the frame does not
+y = t, t+12, ...).  Here rank r of G renders rows y = r + k*G (or, with band = B > 1, the bands r + k*G of B rows:
+north_star's row-tile split, whose 8x8 pixel tiles are 8 adjacent image rows) into a compact [rows, W, 3] uint8 buffer
+on its own GPU (the kernel seeds each pixel with its absolute index x + y*W, main.c:95, so the frame does not
 depend on G), the compact parts are gathered to rank 0 with one collective (torch.distributed over the `nccl`
 backend = RCCL; `gloo` for CPU tests) and rank 0 re-interleaves them with rtc_deinterleave_async.
 
@@ -69,21 +70,50 @@ def pin_rank_near_gpu(device_index: int, threads: int = 1) -> dict:
     return done
 
 
-def rows_per_rank(height: int, world: int) -> int:
+def band_rows(height: int, rank: int, world: int, band: int = 1) -> list[int]:
+    """The image rows rank `rank` of `world` renders, in its compact order: y = rank + k*world (main.c:84 lifted to
+    ranks), or with band B > 1 the bands b = rank + k*world of B rows (rtc.h RtcRenderDesc.rowBand)."""
+    B = max(1, band)
+    return [y for b in range(rank, (height + B - 1) // B, world) for y in range(b * B, min(height, b * B + B))]
+
+
+def copy_rank_rows_to_host(frame_ptr: int, width: int, height: int, rank: int, world: int, dev_ptr: int,
+                           band: int = 1) -> None:
+    """Rank `rank`'s compact rows (device memory) into their places of a page-locked host frame [height, width, 3] with
+    the SDMA engines (rtc_copy_rows_d2h_dma): its full bands as rows of `band` image rows at the band pitch
+    world*band*W*3, then a last partial band -- what rtc_frame_loop's copy thread does."""
+    from . import copy_rows_d2h_dma
+
+    B = max(1, band)
+    rows = len(band_rows(height, rank, world, B))
+    rb = width * 3
+    full, tail = rows // B, rows % B
+    dst = frame_ptr + rank * B * rb
+    if full:
+        copy_rows_d2h_dma(dst, world * B * rb, dev_ptr, B * rb, B * rb, full)
+    if tail:
+        copy_rows_d2h_dma(dst + full * world * B * rb, rb, dev_ptr + full * B * rb, rb, rb, tail)
+
+
+def rows_per_rank(height: int, world: int, band: int = 1) -> int:
     """Rows in the largest part (rank 0's); every rank's compact buffer is padded to this for the gather."""
-    return (height + world - 1) // world
+    return len(band_rows(height, 0, world, band))
 
 
-def rank_config(cfg: RenderConfig, rank: int, world: int) -> RenderConfig:
-    return dataclasses.replace(cfg, row_start=rank, row_stride=world)
+def rank_config(cfg: RenderConfig, rank: int, world: int, band: int = 1) -> RenderConfig:
+    """Rank `rank`'s share: rows y = rank + k*world, or (band > 1) the bands rank + k*world of `band` rows."""
+    B = max(1, band)
+    return dataclasses.replace(cfg, row_start=rank * B, row_stride=world, row_band=B if B > 1 else 0)
 
 
-def interleave_reference(parts: torch.Tensor, height: int) -> torch.Tensor:
-    """Host/CPU statement of the re-interleave (used to check the kernel and the gloo path):
-    out[y] = parts[y % G][y // G]."""
+def interleave_reference(parts: torch.Tensor, height: int, band: int = 1) -> torch.Tensor:
+    """Host/CPU statement of the re-interleave (used to check the kernel and the gloo path): image row y is row
+    band_rows(height, g, G, band).index(y) of part g, g = (y // band) % G."""
     world = parts.shape[0]
+    B = max(1, band)
     ys = torch.arange(height)
-    return parts[ys % world, ys // world]
+    b = ys // B
+    return parts[b % world, (b // world) * B + ys % B]
 
 
 class FrameRenderer:
@@ -91,7 +121,7 @@ class FrameRenderer:
     rank's compact rows; the default uses the HIP kernel through DeviceScene on the current stream."""
 
     def __init__(self, cfg: RenderConfig, render_part: Callable[[RenderConfig, torch.Tensor], None],
-                 device: torch.device, group=None):
+                 device: torch.device, group=None, band: int = 1):
         self.cfg = cfg
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -99,8 +129,9 @@ class FrameRenderer:
         # global rank of the group's rank 0, the gather's destination
         self.root = dist.get_global_rank(group, 0) if (dist.is_initialized() and group is not None) else 0
         self.device = device
-        self.rows = rows_per_rank(cfg.height, self.world)
-        self.cfg_r = rank_config(cfg, self.rank, self.world)
+        self.band = max(1, band)
+        self.rows = rows_per_rank(cfg.height, self.world, self.band)
+        self.cfg_r = rank_config(cfg, self.rank, self.world, self.band)
         self.render_part = render_part
         self.part = torch.zeros((self.rows, cfg.width, 3), dtype=torch.uint8, device=device)
         if self.rank == 0:
@@ -121,9 +152,9 @@ class FrameRenderer:
             return None
         if self.device.type == "cuda":
             deinterleave_async(self.gathered.data_ptr(), self.world, self.rows, self.cfg.width, self.cfg.height,
-                               self.frame.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+                               self.frame.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream, self.band)
         else:
-            self.frame.copy_(interleave_reference(self.gathered, self.cfg.height))
+            self.frame.copy_(interleave_reference(self.gathered, self.cfg.height, self.band))
         return self.frame
 
 
@@ -173,9 +204,10 @@ class SharedHostFrames:
             host_register(self.frames.ctypes.data, self.nbytes)
             self.registered = True
 
-    def rank_rows_ptr(self, b: int, rank: int) -> int:
-        """Where rank `rank`'s first row (y = rank) of frame buffer b lives; the row pitch is world * W * 3."""
-        return self.frames[b].ctypes.data + rank * self.width * 3
+    def rank_rows_ptr(self, b: int, rank: int, band: int = 1) -> int:
+        """Where rank `rank`'s first row (y = rank, or y = rank*band for bands) of frame buffer b lives; the pitch
+        between its consecutive rows (bands) is world * band * W * 3."""
+        return self.frames[b].ctypes.data + rank * max(1, band) * self.width * 3
 
     def close(self, barrier) -> None:
         import os

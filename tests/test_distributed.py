@@ -15,8 +15,8 @@ import torch.multiprocessing as mp
 
 from conftest import load_tris, setup_from_flags
 
-from raytracingc_amd.distributed import (FrameRenderer, SharedHostFrames, interleave_reference, rank_config,
-                                         rows_per_rank)
+from raytracingc_amd.distributed import (FrameRenderer, SharedHostFrames, band_rows, interleave_reference,
+                                         rank_config, rows_per_rank)
 
 W, H, SPP = 40, 23, 2
 
@@ -34,20 +34,20 @@ def _oracle_part(cfg_r, out):
     tris, tonly = load_tris("fsuzane")
     scene, cam, _ = setup_from_flags({})
     d = RtcRenderDesc(cfg_r.width, cfg_r.height, cfg_r.spp, cfg_r.max_bounce, tonly, cfg_r.row_start,
-                      cfg_r.row_stride, 0)
+                      cfg_r.row_stride, 0, cfg_r.row_band)
     col, _, _ = orc.render(tris, None, scene, cam, d, threads=2)
     out.zero_()
     out[: col.shape[0]].copy_(torch.from_numpy(col))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, band=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import raytracingc_amd as rt
 
         cfg = rt.RenderConfig(W, H, SPP, 10, True)
-        fr = FrameRenderer(cfg, _oracle_part, torch.device("cpu"))
+        fr = FrameRenderer(cfg, _oracle_part, torch.device("cpu"), band=band)
         frame = fr()
         if rank == 0:
             q.put(frame.numpy().copy())
@@ -55,14 +55,16 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_frame_equals_single_process(world):
+@pytest.mark.parametrize("world,band", [(2, 1), (3, 1), (2, 8), (3, 4)])
+def test_gloo_frame_equals_single_process(world, band):
+    """Rows (band 1) or bands of rows (north_star's row-tile split) across gloo ranks, gathered to rank 0 and
+    re-interleaved: the single-process frame."""
     import raytracingc_amd as rt
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, band)) for r in range(world)]
     for p in procs:
         p.start()
     frame = q.get(timeout=120)
@@ -121,6 +123,44 @@ def test_parse_cpulist():
 
     assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
     assert parse_cpulist("") == set() and parse_cpulist("5") == {5}
+
+
+def test_band_partition_helpers():
+    """rtc.h rowBand: every image row belongs to exactly one rank; the rows each rank renders (band_rows) are what the
+    C ABI (rtc_rows_selected) and the oracle (oracle_rows_selected) count, in the same order the oracle renders them;
+    the re-interleave statement puts them back."""
+    import ctypes as C
+
+    import oracle.binding as orc
+    import raytracingc_amd as rt
+
+    for h, g, b in [(1080, 8, 8), (1080, 4, 8), (67, 3, 8), (67, 8, 4), (23, 2, 8), (5, 8, 8), (2160, 8, 16), (17, 1, 8)]:
+        got = sorted(y for r in range(g) for y in band_rows(h, r, g, b))
+        assert got == list(range(h)), (h, g, b)
+        assert rows_per_rank(h, g, b) == max(len(band_rows(h, r, g, b)) for r in range(g))
+        for r in range(g):
+            cfg = rank_config(rt.RenderConfig(8, h), r, g, b)
+            d = cfg.desc()
+            n = len(band_rows(h, r, g, b))
+            assert rt.lib().rtc_rows_selected(C.byref(d)) == n, (h, g, b, r)
+            assert orc.lib().oracle_rows_selected(C.byref(d)) == n, (h, g, b, r)
+        parts = torch.zeros((g, rows_per_rank(h, g, b), 2), dtype=torch.int32)
+        for r in range(g):
+            ys = band_rows(h, r, g, b)
+            parts[r, :len(ys), 0] = torch.tensor(ys, dtype=torch.int32)
+        assert torch.equal(interleave_reference(parts, h, b)[:, 0], torch.arange(h, dtype=torch.int32))
+    # the oracle renders a band share's rows exactly as the full frame's same rows (the seed is the absolute pixel)
+    import oracle.binding as orc2
+    from raytracingc_amd._abi import RtcRenderDesc
+
+    tris, tonly = load_tris("complex")
+    scene, cam, _ = setup_from_flags({})
+    Wd, Hd = 24, 37
+    full, facc, _ = orc2.render(tris, None, scene, cam, RtcRenderDesc(Wd, Hd, 2, 10, tonly, 0, 1, 0), threads=4)
+    for r, g, b in [(1, 3, 8), (0, 2, 16), (2, 4, 4)]:
+        ys = band_rows(Hd, r, g, b)
+        col, acc, _ = orc2.render(tris, None, scene, cam, RtcRenderDesc(Wd, Hd, 2, 10, tonly, r * b, g, 0, b), threads=4)
+        assert np.array_equal(col, full[ys]) and np.array_equal(acc.view(np.uint32), facc[ys].view(np.uint32))
 
 
 def test_partition_helpers():

@@ -260,12 +260,14 @@ def test_debug_bounce_integrator(scene, mb, gpu_available):
     assert exact == 1.0  # no environment lookup in this integrator: bit-exact
 
 
-def test_row_partition_and_deinterleave(gpu_available):
-    """Ranks render y = r + k*G into compact buffers; the gathered parts re-interleaved by the kernel equal
-    the single-GPU frame bit for bit (G = 2..8 simulated on one device)."""
+@pytest.mark.parametrize("band", [1, 8, 4])
+def test_row_partition_and_deinterleave(band, gpu_available):
+    """Ranks render y = r + k*G (band 1) or the bands r + k*G of `band` rows (rtc.h rowBand) into compact buffers;
+    the gathered parts re-interleaved by the kernel equal the single-GPU frame bit for bit (G = 2..8 simulated on one
+    device; H = 67 leaves a partial last band)."""
     import torch
 
-    from raytracingc_amd.distributed import rows_per_rank
+    from raytracingc_amd.distributed import rank_config, rows_per_rank
 
     tris, tonly = load_tris("ultracomplex")
     scene, cam, _ = setup_from_flags({})
@@ -274,21 +276,25 @@ def test_row_partition_and_deinterleave(gpu_available):
     ref, _, _ = rt.render(tris, None, scene, cam, cfg)
     ds = rt.DeviceScene(tris, None)
     for G in (2, 3, 4, 8):
-        rows = rows_per_rank(H, G)
+        rows = rows_per_rank(H, G, band)
         parts = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
         for r in range(G):
-            ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, 4, 10, True, row_start=r, row_stride=G),
-                                 parts[r].data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+            rc = rank_config(cfg, r, G, band)
+            if rc.rows() == 0:
+                continue
+            ds.render_rows_async(scene, cam, rc, parts[r].data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-        rt.deinterleave_async(parts.data_ptr(), G, rows, W, H, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        rt.deinterleave_async(parts.data_ptr(), G, rows, W, H, out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                              band)
         torch.cuda.synchronize()
-        assert np.array_equal(out.cpu().numpy(), ref), f"G={G}"
+        assert np.array_equal(out.cpu().numpy(), ref), f"G={G} band={band}"
     ds.close()
 
 
+@pytest.mark.parametrize("band", [1, 8])
 @pytest.mark.parametrize("G", [8, 4])
 @pytest.mark.parametrize("overlap", [False, True])
-def test_small_shares_sum_in_kernel(overlap, G, gpu_available):
+def test_small_shares_sum_in_kernel(overlap, G, band, gpu_available):
     """The bench's 8- and 4-GPU shares of the 1080p x64 headline frame (rows y = r + Gk, 135 / 270 rows: small enough
     that rtc_render_chain sums each pixel's samples itself instead of the deferred pass) equal the single-GPU frame,
     which sums deferred, bit for bit in floats and bytes; with and without frame pipelining (pipelined, consecutive
@@ -300,21 +306,24 @@ def test_small_shares_sum_in_kernel(overlap, G, gpu_available):
     scene, cam, _ = setup_from_flags({})
     W, H = 1920, 1080
     ref, racc, _ = rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, 64, 10, True), want_accum=True)
+    from raytracingc_amd.distributed import band_rows, rank_config, rows_per_rank
+
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.current_stream().cuda_stream
-    rows = (H + G - 1) // G
+    rows = rows_per_rank(H, G, band)
     out = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
     acc = torch.zeros((G, rows, W, 3), dtype=torch.float32, device="cuda")
     for r in range(G):
-        cfg = rt.RenderConfig(W, H, 64, 10, True, row_start=r, row_stride=G, overlap=overlap)
+        cfg = rank_config(rt.RenderConfig(W, H, 64, 10, True, overlap=overlap), r, G, band)
         ds.render_rows_async(scene, cam, cfg, out[r].data_ptr(), acc[r].data_ptr(), None, st)
     torch.cuda.synchronize()
     ds.close()
     o, a = out.cpu().numpy(), acc.cpu().numpy()
     for r in range(G):
-        n = len(range(r, H, G))
-        assert np.array_equal(o[r, :n], ref[r::G]), f"rank {r} bytes"
-        assert np.array_equal(_bits(a[r, :n]), _bits(racc[r::G])), f"rank {r} floats"
+        ys = band_rows(H, r, G, band)
+        n = len(ys)
+        assert np.array_equal(o[r, :n], ref[ys]), f"rank {r} bytes"
+        assert np.array_equal(_bits(a[r, :n]), _bits(racc[ys])), f"rank {r} floats"
 
 
 def test_device_scene_reuse_sizes_counters_timing(gpu_available):
@@ -484,8 +493,9 @@ def test_spp_not_multiple_of_64(variant, gpu_available):
     assert st["segments"] == oseg
 
 
+@pytest.mark.parametrize("band", [0, 8])
 @pytest.mark.parametrize("name", ["complex", "ultracomplex"])
-def test_render_multi_rccl_equals_render(name, gpu_available):
+def test_render_multi_rccl_equals_render(name, band, gpu_available):
     """rtc_render_multi over every visible device (ncclCommInitAll clique, ncclGather to device 0, re-interleave,
     one D2H) == rtc_render bit for bit, colors and floats; the frame time covers the frame's arrival on the
     host.  On a one-GPU box this runs the whole RCCL path with a clique of one."""
@@ -493,7 +503,8 @@ def test_render_multi_rccl_equals_render(name, gpu_available):
     scene, cam, _ = setup_from_flags({})
     cfg = rt.RenderConfig(160, 90, 8, 10, True)
     a, fa, sa = rt.render(tris, None, scene, cam, cfg, want_accum=True)
-    b, fb, sb = rt.render_multi(tris, None, scene, cam, cfg, rt.device_count(), want_accum=True)
+    b, fb, sb = rt.render_multi(tris, None, scene, cam, rt.RenderConfig(160, 90, 8, 10, True, row_band=band),
+                                rt.device_count(), want_accum=True)
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
     assert sa["segments"] == sb["segments"]
     assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
@@ -764,15 +775,16 @@ def _shm_frame(nbytes):
     return mm, arr
 
 
+@pytest.mark.parametrize("band", [1, 8])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (121, 67)])
-def test_strided_row_copies_build_host_frame(W, H, gpu_available):
+def test_strided_row_copies_build_host_frame(W, H, band, gpu_available):
     """The multi-GPU host-frame path: ranks' compact rows y = r + k*G (G = 2..8 simulated on one device), each
     copied by rtc_copy_rows_d2h_dma straight into its places of one host frame (pitch G*W*3; SDMA sub-window copy,
     or per-row copies when W*3 is not a multiple of 4) -- into hipHostMalloc'd memory and into a registered
     shared-memory frame -- equal the single-GPU host frame byte for byte (main.c:84, :285-302)."""
     import torch
 
-    from raytracingc_amd.distributed import rows_per_rank
+    from raytracingc_amd.distributed import copy_rank_rows_to_host, rank_config, rows_per_rank
 
     tris, _ = load_tris("ultracomplex")
     scene, cam, _ = setup_from_flags({})
@@ -783,18 +795,18 @@ def test_strided_row_copies_build_host_frame(W, H, gpu_available):
     mm, shm = _shm_frame(H * W * 3)
     try:
         for G in (2, 3, 4, 8):
-            rows = rows_per_rank(H, G)
+            rows = rows_per_rank(H, G, band)
             parts = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
             for r in range(G):
-                ds.render_rows_async(scene, cam, rt.RenderConfig(W, H, 4, 10, True, row_start=r, row_stride=G),
-                                     parts[r].data_ptr(), stream=st.cuda_stream)
+                rc = rank_config(cfg, r, G, band)
+                if rc.rows():
+                    ds.render_rows_async(scene, cam, rc, parts[r].data_ptr(), stream=st.cuda_stream)
             torch.cuda.synchronize()
             pinned = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True)
             shm[:] = 0
             for r in range(G):
-                n = len(range(r, H, G))
                 for dst in (pinned.data_ptr(), shm.ctypes.data):
-                    rt.copy_rows_d2h_dma(dst + r * W * 3, G * W * 3, parts[r].data_ptr(), W * 3, W * 3, n)
+                    copy_rank_rows_to_host(dst, W, H, r, G, parts[r].data_ptr(), band)
             assert np.array_equal(pinned.numpy(), ref), f"G={G} pinned"
             assert np.array_equal(shm.reshape(H, W, 3), ref), f"G={G} shm"
     finally:
@@ -804,15 +816,17 @@ def test_strided_row_copies_build_host_frame(W, H, gpu_available):
         ds.close()
 
 
+@pytest.mark.parametrize("band", [0, 8])
 @pytest.mark.parametrize("name", ["complex", "ultracomplex"])
-def test_render_multi_host_rows_equals_render(name, gpu_available):
-    """rtc_render_multi with RTC_F_HOST_ROWS (no gather: every device copies its rows into the host frame) ==
-    rtc_render bit for bit, colors and floats, same paths."""
+def test_render_multi_host_rows_equals_render(name, band, gpu_available):
+    """rtc_render_multi with RTC_F_HOST_ROWS (no gather: every device copies its rows -- or bands of 8 rows -- into the
+    host frame) == rtc_render bit for bit, colors and floats, same paths."""
     tris, tonly = load_tris(name)
     scene, cam, _ = setup_from_flags({})
     cfg = rt.RenderConfig(160, 90, 8, 10, True)
     a, fa, sa = rt.render(tris, None, scene, cam, cfg, want_accum=True)
-    b, fb, sb = rt.render_multi(tris, None, scene, cam, rt.RenderConfig(160, 90, 8, 10, True, host_rows=True),
+    b, fb, sb = rt.render_multi(tris, None, scene, cam,
+                                rt.RenderConfig(160, 90, 8, 10, True, host_rows=True, row_band=band),
                                 rt.device_count(), want_accum=True)
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
     assert sa["segments"] == sb["segments"]
@@ -839,15 +853,20 @@ def test_frame_loop_pipelined_host_frames(gpu_available):
     for h in host:
         assert np.array_equal(h.numpy(), ref)
     G = 3
+    from raytracingc_amd.distributed import rank_config
+
     mm, shm = _shm_frame(2 * H * W * 3)
     try:
         frames = shm.reshape(2, H, W, 3)
-        for r in range(G):
-            cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
-            ds.frame_loop(scene, cam, cfg, [d.data_ptr() for d in dev[:2]],
-                          [frames[b].ctypes.data + r * W * 3 for b in range(2)], G * W * 3, 4, st.cuda_stream)
-        for b in range(2):
-            assert np.array_equal(frames[b], ref), f"buffer {b}"
+        for band in (1, 8):  # single rows, then bands of 8 rows (360 = 45 bands: a rank's last band may be cut)
+            shm[:] = 0
+            for r in range(G):
+                cfg = rank_config(rt.RenderConfig(W, H, spp, 10, True), r, G, band)
+                ds.frame_loop(scene, cam, cfg, [d.data_ptr() for d in dev[:2]],
+                              [frames[b].ctypes.data + r * band * W * 3 for b in range(2)], G * band * W * 3, 4,
+                              st.cuda_stream)
+            for b in range(2):
+                assert np.array_equal(frames[b], ref), f"buffer {b} band {band}"
     finally:
         rt.host_unregister(shm.ctypes.data)
         del frames, shm
@@ -855,62 +874,65 @@ def test_frame_loop_pipelined_host_frames(gpu_available):
     ds.close()
 
 
+@pytest.mark.parametrize("band", [1, 8])
 @pytest.mark.parametrize("scene,spp,G", [("complex", 64, 4), ("ultracomplex", 64, 8), ("ultracomplex", 256, 8)])
-def test_4k_row_shares_assemble_bit_exact(scene, spp, G, gpu_available):
+def test_4k_row_shares_assemble_bit_exact(scene, spp, G, band, gpu_available):
     """BASELINE.json C4 (complex 3840x2160x64 over 4 GPUs), NS (ultracomplex 4K x64) and C5 (ultracomplex 4K x256)
-    over 8 GPUs: every rank's share (rows y = r + k*G, main.c:84 lifted to GPUs; 540 / 270 rows of 3840, so the
-    deferred-sum path with 8x8 tiles spanning 32-64 image rows) rendered on one device, assembled two ways -- the
-    RCCL path's re-interleave on the device (rtc_deinterleave_async) and the host-frame path's strided SDMA copies
-    into one pinned frame (rtc_copy_rows_d2h_dma) -- equals the single-GPU 4K frame bit for bit, bytes and floats;
-    the last share equals the oracle's render of the same rows (rowStart, rowStride) bit for bit with the same
+    over 8 GPUs: every rank's share (rows y = r + k*G, main.c:84 lifted to GPUs, or the bands r + k*G of 8 rows:
+    north_star's row-tile split; 540 / 270 rows of 3840, so the deferred-sum path) rendered on one device, assembled
+    two ways -- the RCCL path's re-interleave on the device (rtc_deinterleave_async / _bands_async) and the host-frame
+    path's strided SDMA copies into one pinned frame (rtc_copy_rows_d2h_dma) -- equals the single-GPU 4K frame bit for
+    bit, bytes and floats; the last share equals the oracle's render of the same rows bit for bit with the same
     paths; and the pipelined per-rank frame loop the bench runs (rtc_frame_loop, RTC_F_OVERLAP) builds the same
     host frame."""
     import torch
 
-    from raytracingc_amd.distributed import rows_per_rank
+    from raytracingc_amd.distributed import band_rows, copy_rank_rows_to_host, rank_config, rows_per_rank
 
     tris, tonly = load_tris(scene)
     sc, cam, _ = setup_from_flags({})
     W, H = 3840, 2160
-    ref, racc, _ = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True), want_accum=True)
+    full = rt.RenderConfig(W, H, spp, 10, True)
+    ref, racc, _ = rt.render(tris, None, sc, cam, full, want_accum=True)
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.current_stream().cuda_stream
-    rows = rows_per_rank(H, G)
+    rows = rows_per_rank(H, G, band)
     parts = torch.zeros((G, rows, W, 3), dtype=torch.uint8, device="cuda")
     accs = torch.zeros((G, rows, W, 3), dtype=torch.float32, device="cuda")
     for r in range(G):
-        cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
+        cfg = rank_config(full, r, G, band)
         assert cfg.rows() * W > 600000  # not a small share: deferred sums (rtc_accumulate_samples)
         ds.render_rows_async(sc, cam, cfg, parts[r].data_ptr(), accs[r].data_ptr(), None, st)
     out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-    rt.deinterleave_async(parts.data_ptr(), G, rows, W, H, out.data_ptr(), st)
+    rt.deinterleave_async(parts.data_ptr(), G, rows, W, H, out.data_ptr(), st, band)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref), "device re-interleave"
     pinned = torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True)
     for r in range(G):
-        rt.copy_rows_d2h_dma(pinned.data_ptr() + r * W * 3, G * W * 3, parts[r].data_ptr(), W * 3, W * 3,
-                             len(range(r, H, G)))
+        copy_rank_rows_to_host(pinned.data_ptr(), W, H, r, G, parts[r].data_ptr(), band)
     assert np.array_equal(pinned.numpy(), ref), "strided SDMA host frame"
     a = accs.cpu().numpy()
     for r in range(G):
-        n = len(range(r, H, G))
-        assert np.array_equal(_bits(a[r, :n]), _bits(racc[r::G])), f"rank {r} floats"
+        ys = band_rows(H, r, G, band)
+        assert np.array_equal(_bits(a[r, :len(ys)]), _bits(racc[ys])), f"rank {r} floats"
     # the pipelined per-rank loop of bench.py, every rank's frames into one pinned host frame pair
     host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     dev = [torch.zeros((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     lst = torch.cuda.Stream()
     for r in range(G):
-        cfg = rt.RenderConfig(W, H, spp, 10, True, row_start=r, row_stride=G)
-        ds.frame_loop(sc, cam, cfg, [d.data_ptr() for d in dev], [h.data_ptr() + r * W * 3 for h in host], G * W * 3,
-                      3, lst.cuda_stream)
+        cfg = rank_config(full, r, G, band)
+        ds.frame_loop(sc, cam, cfg, [d.data_ptr() for d in dev], [h.data_ptr() + r * band * W * 3 for h in host],
+                      G * band * W * 3, 3, lst.cuda_stream)
     for h in host:
         assert np.array_equal(h.numpy(), ref), "frame loop host frame"
     ds.close()
     r0 = G - 1
-    ocol, oacc, oseg = orc.render(tris, None, sc, cam, RtcRenderDesc(W, H, spp, 10, tonly, r0, G, 0), threads=16)
-    n = len(range(r0, H, G))
+    rc = rank_config(full, r0, G, band)
+    ocol, oacc, oseg = orc.render(tris, None, sc, cam, rc.desc(), threads=16)
+    n = rc.rows()
+    assert n == len(band_rows(H, r0, G, band)) == oacc.shape[0]
     assert np.array_equal(_bits(a[r0, :n]), _bits(oacc)) and np.array_equal(parts[r0, :n].cpu().numpy(), ocol)
-    _, _, sr = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True, row_start=r0, row_stride=G))
+    _, _, sr = rt.render(tris, None, sc, cam, rc)
     assert sr["segments"] == oseg
 
 

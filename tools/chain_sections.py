@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """Section cycles of rtc_render_chain from the diagnostic build (librtc_diag.so, s_memtime stamps summed over
-waves), on the BASELINE frame (or another scene: chain_sections.py fsuzane).  Not part of the product."""
+waves), on the BASELINE frame (or another scene: chain_sections.py fsuzane).  Not part of the product.
+
+Round 5: the top-level sections are uniform marks that tile each wave's lifetime (DMARK: every cycle from the kernel's
+first mark to its last lands in exactly one of them, so `covered` is ~1 by construction); the finer sections nest
+inside them (BEGIN/END pairs): the first-bounce table, cluster cull, pair build and pair passes inside the bounce
+trace, the hit branch and the environment inside the shading."""
 import ctypes as C
 import json
 import os
@@ -13,27 +18,45 @@ os.environ["RTC_LIB_PATH"] = os.environ.get("RTC_DIAG_LIB") or os.path.join(REPO
 import raytracingc_amd as rt  # noqa: E402
 from conftest import load_tris  # noqa: E402
 
+NS = 24
+TOP = {19: "prologue", 15: "item_setup", 0: "window_setup", 1: "primary_trace", 17: "bounce_trace", 16: "shading",
+       7: "walk_and_sums", 18: "item_tail"}
+NESTED = {14: ("bounce_trace", "first_bounce_table"), 3: ("bounce_trace", "cluster_cull"),
+          4: ("bounce_trace", "pair_build"), 5: ("bounce_trace", "pair_passes"), 2: ("shading", "hit"),
+          6: ("shading", "environment")}
 scene_name = sys.argv[1] if len(sys.argv) > 1 else "ultracomplex"
+W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 tris, _ = load_tris(scene_name)
 L = rt.lib()
 L.rtc_diag_sections.argtypes = [C.c_void_p, C.c_int]
-out = (C.c_ulonglong * 16)()
-names = ["rng_setup", "primary_trace", "hit_shading", "cluster_cull", "pair_build", "pair_passes", "env", "walk"]
+out = (C.c_ulonglong * NS)()
 for hoist in (False, True):
-    cfg = rt.RenderConfig(1920, 1080, 64, 10, True, hoist=hoist)
-    rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+    # pipelined launches like the bench's timed frames (in-kernel sums on the alternating streams), one at a time
+    import torch
+
+    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, overlap=True)
+    ds = rt.DeviceScene(tris, None)
+    buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    for _ in range(3):
+        ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, buf.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
     L.rtc_diag_sections(out, 1)
-    _, _, st = rt.render(tris, None, rt.default_scene(), rt.camera_basis(), cfg)
+    ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, buf.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
     L.rtc_diag_sections(out, 1)
-    tot = sum(out[i] for i in range(8))
+    ds.close()
+    life = out[13]
+    top = {n: int(out[i]) for i, n in TOP.items()}
+    nested = {f"{p}/{n}": int(out[i]) for i, (p, n) in NESTED.items()}
     it, alive, act, win, used = (out[i] for i in range(8, 13))
-    print(json.dumps({"hoist": hoist, "iterations": it, "lane_utilisation": round(alive / max(1, 64 * it), 4),
-                      "window_lanes_per_window": round(act / max(1, win), 2), "used_lanes_share": round(used / max(1, act), 4),
+    print(json.dumps({"scene": scene_name, "W": W, "H": H, "spp": SPP, "hoist": hoist, "iterations": it,
+                      "lane_utilisation": round(alive / max(1, 64 * it), 4),
+                      "window_lanes_per_window": round(act / max(1, win), 2),
+                      "used_lanes_share": round(used / max(1, act), 4),
                       "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
-    print(json.dumps({"hoist": hoist, "render_ms": round(st["render_ms"], 3),
-                      "share": {n: round(out[i] / tot, 4) for i, n in enumerate(names)},
-                      "cycles": {n: int(out[i]) for i, n in enumerate(names)},
-                      # 13: whole wave lifetime, 14: first-bounce tables (cluster terms, reach), 15: item fetch and
-                      # pixel setup -- the sections above cover tot / lifetime of the waves' cycles
-                      "wave_cycles": int(out[13]), "table_build": int(out[14]), "item_setup": int(out[15]),
-                      "covered": round((tot + out[14] + out[15]) / max(1, out[13]), 4)}), flush=True)
+    print(json.dumps({"hoist": hoist, "wave_cycles": int(life),
+                      "share": {n: round(v / max(1, life), 4) for n, v in top.items()},
+                      "nested_share": {n: round(v / max(1, life), 4) for n, v in nested.items()},
+                      "cycles": top, "nested_cycles": nested,
+                      "covered": round(sum(top.values()) / max(1, life), 4)}), flush=True)
