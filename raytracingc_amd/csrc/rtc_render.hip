@@ -1900,7 +1900,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
             } else {
 #pragma unroll RTC_SKY_UNROLL
                 for (int s = 0; s < P.spp; ++s) {
-#ifdef RTC_AB_CHEAP_ENV_SKY /* timing experiment only (the sky pass's environment cost) */
+#if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the sky pass's environment cost) */
                     const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(px.dir.y + (float)s * 1e-9f, 0.f));
 #else
                     const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
@@ -1949,6 +1949,89 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
                 P.accum[3 * o + 2] = acc.z;
             }
         }
+    }
+    flush_counters(P, segCalls, segTraced, 0ull, lane);
+}
+
+/* Sky pixels by row strips (round 5, RTC_SKY_ROWS): each wave takes 64 consecutive pixels of one launch row (workgroups of
+ * kSkyWaves waves: kSkyWaves consecutive rows), so a strip of Color is 192 B = three whole 64-B lines when the row starts
+ * on a line (every BASELINE width: 1920 * 3 and 3840 * 3 are multiples of 64), written by twelve 16-B stores staged in
+ * LDS.  The 8x8-tile waves wrote 24-B tile rows that straddle lines shared with the neighbouring tiles' waves, so every
+ * line was written back partially two or three times (sky WRITE_SIZE 12.0 MB per 1080p launch for 6.0 MB of Color,
+ * VERDICT r04 #5).  A strip holding geometry pixels (rtc_render_chain writes those, maybe concurrently) or cut by the frame
+ * edge writes its sky pixels' bytes only.  Same pixels, same per-sample environment loop, same values. */
+#ifndef RTC_SKY_ROWS
+#define RTC_SKY_ROWS 1
+#endif
+template <int kSkyWaves>
+__global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky_rows(
+    RenderParams P, const unsigned *__restrict__ tileW)
+{
+    static_assert(kSkyWaves == 4 || kSkyWaves == 1, "one or four row strips per workgroup");
+    __shared__ PowTablesLds sPow;
+    __shared__ __attribute__((aligned(16))) unsigned char sStrip[kSkyWaves][192];
+    sPow.fill(threadIdx.x);
+    __syncthreads();
+    sPow.attach(P.env);
+    const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;
+    unsigned segCalls = 0, segTraced = 0;
+    const int r = (int)blockIdx.y * kSkyWaves + __builtin_amdgcn_readfirstlane(lw); /* launch row (wave-uniform) */
+    const int x = (int)blockIdx.x * 64 + lane;
+    bool valid = r < P.rows && x < P.width;
+    /* the pixel's tile: pixels with a primary candidate are rtc_render_chain's (pixMask bit (row % 8) * 8 + x % 8) */
+    if (valid) {
+        const int t = (r >> 3) * (P.blocksX * 2) + (x >> 3);
+        const bool geo = tileW[t] > 0 && ((P.pixMask[t] >> (((r & 7) << 3) | (x & 7))) & 1ull);
+        valid = !geo;
+    }
+    const unsigned long long mine = __ballot(valid);
+    if (mine == 0ull)
+        return;
+    const int y = launch_row_y(P, r);
+    const V3 dir = primary_dir(P, x, y);
+    V3 acc{0.f, 0.f, 0.f};
+    if (valid && P.spp > 0 && P.maxBounce > 0) {
+        /* see rtc_render_sky: hoisted mode evaluates the primary ray's miss once, faithful mode every sample */
+        if (P.hoist) {
+            const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f}));
+            for (int s = 0; s < P.spp; ++s)
+                acc = add(acc, mul(l, P.invSpp));
+        } else {
+#pragma unroll RTC_SKY_UNROLL
+            for (int s = 0; s < P.spp; ++s) {
+#if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the environment's cost) */
+                const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y + (float)s * 1e-9f, 0.f));
+#else
+                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f})); /* raytracing.c:291 */
+#endif
+                acc = add(acc, mul(l, P.invSpp)); /* main.c:99 */
+            }
+        }
+        segCalls = (unsigned)P.spp;
+        segTraced = P.hoist ? 1u : (unsigned)P.spp;
+    }
+    /* vec3ToColor (raytracing.c:11-15, main.c:101) */
+    const unsigned char c0 = float_to_u8(acc.x), c1 = float_to_u8(acc.y), c2 = float_to_u8(acc.z);
+    unsigned char *const rowp = P.colors + 3 * ((size_t)r * (size_t)P.width + (size_t)blockIdx.x * 64);
+    const bool whole = mine == ~0ull && ((uintptr_t)rowp & 15u) == 0u; /* wave-uniform */
+    if (whole) {
+        unsigned char *st = sStrip[lw];
+        st[3 * lane] = c0;
+        st[3 * lane + 1] = c1;
+        st[3 * lane + 2] = c2;
+        wave_lds_sync();
+        if (lane < 12)
+            ((uint4 *)rowp)[lane] = ((const uint4 *)st)[lane];
+    } else if (valid) {
+        rowp[3 * lane] = c0;
+        rowp[3 * lane + 1] = c1;
+        rowp[3 * lane + 2] = c2;
+    }
+    if (valid && P.accum) {
+        const size_t o = 3 * ((size_t)r * (size_t)P.width + (size_t)x);
+        P.accum[o] = acc.x;
+        P.accum[o + 1] = acc.y;
+        P.accum[o + 2] = acc.z;
     }
     flush_counters(P, segCalls, segTraced, 0ull, lane);
 }
@@ -2501,7 +2584,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0, segSpec = 0;
 #ifdef RTC_DIAG
-    unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0;
+    unsigned long long dIters = 0, dAlive = 0, dAct = 0, dWindows = 0, dUsed = 0, dIters2 = 0, dAlive2 = 0;
 #endif
     /* the sub-lists' inclusive prefix counts, lane l < kGeoLists holding sub-list l's, loaded once per wave: an
      * item's sub-list is then a ballot, not a chain of dependent count loads as a wave's items pass the sub-lists */
@@ -2619,6 +2702,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #ifdef RTC_DIAG
                 dIters++;
                 dAlive += (unsigned long long)__popcll(__ballot(alive));
+                if (iter >= 2) {
+                    dIters2++;
+                    dAlive2 += (unsigned long long)__popcll(__ballot(alive));
+                }
 #endif
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
@@ -2643,7 +2730,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
                     }
-                    DMARK(dcur, 17); /* bounce trace (14 table, 3 cull, 4 pair build, 5 pair passes inside) */
+                    DMARK(dcur, bounce1 ? 17 : 20); /* bounce trace: the first bounce (17), later ones (20); 14 table, 3
+                                                     * cull, 4 pair build, 5 pair passes inside */
                 }
 #if RTC_DRAW_TABLE
                 /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
@@ -2722,7 +2810,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     if (endSample)
                         alive = false;
                 }
-                DMARK(dcur, 16); /* shading (2 hit, 6 environment inside) */
+                DMARK(dcur, iter < 2 ? 16 : 21); /* shading (2 hit, 6 environment inside); 21: after later bounces */
             }
             (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
@@ -2838,7 +2926,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     DMARK(dcur, 15);
 #ifdef RTC_DIAG
     DSECT_END(dtot, 13);
-    if (lane < 8 || (lane >= 13 && lane < kDiagSects))
+    if (lane < 8 || (lane >= 13 && lane < 22))
         atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
     /* [8] bounce-loop iterations, [9] live lanes summed over them, [10] window lanes, [11] windows, [12] lanes
      * whose sample was used */
@@ -2848,6 +2936,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         atomicAdd(&g_rtc_sect[10], dAct);
         atomicAdd(&g_rtc_sect[11], dWindows);
         atomicAdd(&g_rtc_sect[12], dUsed);
+        atomicAdd(&g_rtc_sect[22], dIters2); /* [22] iterations of later bounces, [23] their live lanes */
+        atomicAdd(&g_rtc_sect[23], dAlive2);
     }
 #endif
     if (counting)
@@ -3218,7 +3308,14 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             }
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky0, skyStream));
-            if (smallShare && (size_t)d->width * (size_t)rows > 400000)
+            const bool skyWide = smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
+            if (RTC_SKY_ROWS && skyWide)
+                hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0,
+                                   skyStream, P, (const unsigned *)tileW);
+            else if (RTC_SKY_ROWS)
+                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, skyStream, P,
+                                   (const unsigned *)tileW);
+            else if (skyWide)
                 hipLaunchKernelGGL(rtc_render_sky<4>, grid, dim3(256), 0, skyStream, P, (const unsigned *)tileW);
             else
                 hipLaunchKernelGGL(rtc_render_sky<1>, dim3(grid.x * 2, grid.y * 2), dim3(64), 0, skyStream, P,

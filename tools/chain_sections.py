@@ -20,10 +20,10 @@ from conftest import load_tris  # noqa: E402
 
 NS = 24
 TOP = {19: "prologue", 15: "item_setup", 0: "window_setup", 1: "primary_trace", 17: "bounce_trace", 16: "shading",
-       7: "walk_and_sums", 18: "item_tail"}
-NESTED = {14: ("bounce_trace", "first_bounce_table"), 3: ("bounce_trace", "cluster_cull"),
-          4: ("bounce_trace", "pair_build"), 5: ("bounce_trace", "pair_passes"), 2: ("shading", "hit"),
-          6: ("shading", "environment")}
+       20: "later_bounce_trace", 21: "later_shading", 7: "walk_and_sums", 18: "item_tail"}
+NESTED = {14: ("bounce_trace", "first_bounce_table"), 3: ("*bounce_trace", "cluster_cull"),
+          4: ("*bounce_trace", "pair_build"), 5: ("*bounce_trace", "pair_passes"), 2: ("*shading", "hit"),
+          6: ("*shading", "environment")}
 scene_name = sys.argv[1] if len(sys.argv) > 1 else "ultracomplex"
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 tris, _ = load_tris(scene_name)
@@ -54,7 +54,9 @@ for hoist in (False, True):
                       "lane_utilisation": round(alive / max(1, 64 * it), 4),
                       "window_lanes_per_window": round(act / max(1, win), 2),
                       "used_lanes_share": round(used / max(1, act), 4),
-                      "iterations_per_window": round(it / max(1, win), 2)}), flush=True)
+                      "iterations_per_window": round(it / max(1, win), 2),
+                      "later_iterations": int(out[22]),
+                      "later_lane_utilisation": round(out[23] / max(1, 64 * out[22]), 4)}), flush=True)
     print(json.dumps({"hoist": hoist, "wave_cycles": int(life),
                       "share": {n: round(v / max(1, life), 4) for n, v in top.items()},
                       "nested_share": {n: round(v / max(1, life), 4) for n, v in nested.items()},
