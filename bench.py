@@ -264,6 +264,11 @@ def main():
     ap.add_argument("--cpu-budget-samples", type=float, default=1.4e8,
                     help="CPU baseline sample size (W*H*spp); the metric's config is rendered whole")
     ap.add_argument("--no-extras", action="store_true", help="skip the hoisted / no-tile-cull / latency extras")
+    ap.add_argument("--band", default="auto",
+                    help="N > 1 partition: rows per interleaved band (1: rows y = r + kN as main.c:84; 8: north_star's "
+                         "row-tile split, bands of 8 rows).  auto: the faster one per frame size as measured on MI355X "
+                         "(profiles/r05_*_scale*: 1080p rows (the 8-row bands' 1/8 shares are less balanced: 4.46x vs "
+                         "4.50x), 4K bands of 8 (6.69x vs 6.48x))")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: process group backend.  nccl (= RCCL, the default) needs a GPU per rank; gloo is an "
                          "explicit rehearsal mode in which ranks may share GPUs (no RCCL leg; the line then reports "
@@ -327,7 +332,10 @@ def main():
     cam = rt.camera_basis()
     ds = rt.DeviceScene(tris, None, device=gpu)
     seg = torch.zeros(rt.RTC_SEGMENT_COUNTERS, dtype=torch.int64, device=dev)
-    rows = rows_per_rank(H, world)
+    band = (8 if H >= 2160 else 1) if args.band == "auto" else max(1, int(args.band))
+    if world == 1:
+        band = 1  # (a whole frame: no partition)
+    rows = rows_per_rank(H, world, band)
     stream = torch.cuda.Stream(dev)
     nbuf = 3
     # this rank's compact rows of each frame in HBM; the host frames: pinned (N = 1) or node-shared (N > 1)
@@ -335,16 +343,16 @@ def main():
     shared = None
     if multi:
         shared = SharedHostFrames(f"rtc_bench_{os.environ.get('MASTER_PORT', '0')}", nbuf, H, W, local, barrier)
-        host_ptr = [shared.rank_rows_ptr(b, rank) for b in range(nbuf)]
+        host_ptr = [shared.rank_rows_ptr(b, rank, band) for b in range(nbuf)]
         host_frame = lambda b: shared.frames[b]  # noqa: E731
     else:
         host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
         host_ptr = [h.data_ptr() + rank * W * 3 for h in host]
         host_frame = lambda b: host[b].numpy()  # noqa: E731
-    pitch = world * W * 3
+    pitch = world * band * W * 3  # between a rank's consecutive rows (bands) in the host frame
 
     cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
-    cfg_r = rank_config(cfg_joined, rank, world)
+    cfg_r = rank_config(cfg_joined, rank, world, band)
 
     def loop(cfg, frames, cams=None):
         return ds.frame_loop(scene, cams or cam, cfg, [t.data_ptr() for t in dev_rows], host_ptr, pitch, frames,
@@ -418,7 +426,7 @@ def main():
 
     extras = {}
     if multi and backend == "nccl":
-        extras["rccl_device_frame"] = rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev,
+        extras["rccl_device_frame"] = rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev, band,
                                                         barrier, allreduce_max)
     if not args.no_extras:
         # device-only frames (left in HBM), the bit-exact hoisted mode, the brute-force primary segments
@@ -492,8 +500,10 @@ def main():
             "data": f"reference scene {scene_name}.obj (Triangle[] from the reference loader, tests/golden/scenes), "
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
-                       "max_bounce": 10, "triangles": T,
-                       "parallelism": f"rows mod {world}; each rank SDMA-copies its rows into the shared host frame"
+                       "max_bounce": 10, "triangles": T, "row_band": band,
+                       "parallelism": (f"rows mod {world}" if band == 1 else
+                                       f"bands of {band} rows mod {world} (row-tile split)")
+                                      + "; each rank SDMA-copies its rows into the shared host frame"
                                       + ("; RCCL gather to rank 0's GPU measured beside it (rccl_device_frame)"
                                          if backend == "nccl" else "")
                                       + (f"; REHEARSAL: {world} gloo ranks on {n_phys} GPU(s), no RCCL leg, not a "
@@ -585,7 +595,7 @@ def dataclasses_replace(cfg, **kw):
     return dataclasses.replace(cfg, **kw)
 
 
-def rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev, barrier, allreduce_max):
+def rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank, dev, band, barrier, allreduce_max):
     """N > 1, every rank on its own GPU: the device-frame path -- each frame's parts gathered to rank 0's GPU over
     xGMI (torch.distributed `nccl` = RCCL) and re-interleaved there (rtc_deinterleave_async), pipelined like the
     host-frame loop (render on one stream, the gather on another after the frame event).  Returns its timing and
@@ -616,7 +626,8 @@ def rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank
         with torch.cuda.stream(gst):
             dist.gather(parts[b], gather_list=list(gathered[b].unbind(0)) if rank == 0 else None, dst=0)
             if rank == 0:
-                rt.deinterleave_async(gathered[b].data_ptr(), world, rows, W, H, frames[b].data_ptr(), gst.cuda_stream)
+                rt.deinterleave_async(gathered[b].data_ptr(), world, rows, W, H, frames[b].data_ptr(), gst.cuda_stream,
+                                      band)
         done = torch.cuda.Event()
         done.record(gst)
         free[b] = done
@@ -636,7 +647,7 @@ def rccl_device_frame(args, tris, ds, scene, cam, cfg_r, rows, W, H, world, rank
            "what": "frame gathered into rank 0's HBM over RCCL (ncclGather via torch.distributed) and re-interleaved; "
                    "no D2H"}
     if rank == 0:
-        ref1, _, _ = rt.render(tris, None, scene, cam, dataclasses_replace(cfg_r, row_start=0, row_stride=1),
+        ref1, _, _ = rt.render(tris, None, scene, cam, dataclasses_replace(cfg_r, row_start=0, row_stride=1, row_band=0),
                                device=dev.index)
         out["frame_equals_1gpu_render"] = bool(np.array_equal(frames[(args.steps - 1) % nbuf].cpu().numpy(), ref1))
     return out

@@ -30,7 +30,11 @@ for s in $steps; do
       done ;;
     scale)
       step scale1080_$tag 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
-      step scale4k_$tag 200 python tools/scale_probe.py 5 3840 2160 64 overlap || exit $? ;;
+      step scale4k_$tag 200 python tools/scale_probe.py 5 3840 2160 64 overlap || exit $?
+      export SCALE_BAND=8
+      step scale1080_band8_$tag 200 python tools/scale_probe.py 5 1920 1080 64 overlap || exit $?
+      step scale4k_band8_$tag 200 python tools/scale_probe.py 5 3840 2160 64 overlap || exit $?
+      unset SCALE_BAND ;;
     loops)
       cd /tmp
       step loop1_$tag 120 rocprofv3 --kernel-trace --stats -d "$OUT/loop1_$tag" -o run --output-format csv -- python3 "$R/tools/frame_loop.py" 40 overlap 1 || exit $?
@@ -42,7 +46,9 @@ for s in $steps; do
       for n in 2 8; do
         step rehearse${n}_$tag 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
           --master-port $((29500 + n)) bench.py --gpus $n --backend gloo --steps 20 --warmup 3 --no-cpu-baseline --no-extras || exit $?
-      done ;;
+      done
+      step rehearse8_band8_$tag 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29518 bench.py --gpus 8 --band 8 --backend gloo --steps 20 --warmup 3 --no-cpu-baseline --no-extras || exit $? ;;
     bench) step bench_$tag 400 python bench.py || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
