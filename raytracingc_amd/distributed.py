@@ -198,6 +198,7 @@ class SharedHostFrames:
         os.close(fd)
         self.frames = np.frombuffer(self.mm, np.uint8).reshape(nbuf, height, width, 3)
         self.frames.reshape(-1)[::4096] = 0  # fault the pages in before page-locking them
+        barrier()  # (no rank writes its rows before every rank's fault-in stores are done)
         if register:
             from . import host_register
 

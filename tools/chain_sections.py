@@ -34,7 +34,8 @@ for hoist in (False, True):
     # pipelined launches like the bench's timed frames (in-kernel sums on the alternating streams), one at a time
     import torch
 
-    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, overlap=True)
+    park = {"": None, "1": True, "0": False}[os.environ.get("RTC_SECT_PARK", "")]
+    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, overlap=True, park=park)
     ds = rt.DeviceScene(tris, None)
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
     st = torch.cuda.Stream()
