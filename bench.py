@@ -269,9 +269,6 @@ def main():
                          "row-tile split, bands of 8 rows).  auto: the faster one per frame size as measured on MI355X "
                          "(profiles/r05_*_scale*: 1080p rows (the 8-row bands' 1/8 shares are less balanced: 4.46x vs "
                          "4.50x), 4K bands of 8 (6.69x vs 6.48x))")
-    ap.add_argument("--park", default="auto", choices=["auto", "on", "off"],
-                    help="rtc_render_chain's parking of windows that bounce again (RTC_F_PARK / RTC_F_NO_PARK; same "
-                         "frame): auto = the scene's default (rtc_scene_upload's probe)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: process group backend.  nccl (= RCCL, the default) needs a GPU per rank; gloo is an "
                          "explicit rehearsal mode in which ranks may share GPUs (no RCCL leg; the line then reports "
@@ -354,7 +351,7 @@ def main():
         host_frame = lambda b: host[b].numpy()  # noqa: E731
     pitch = world * band * W * 3  # between a rank's consecutive rows (bands) in the host frame
 
-    cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly), park={"auto": None, "on": True, "off": False}[args.park])
+    cfg_joined = rt.RenderConfig(W, H, spp, 10, bool(tonly))
     cfg_r = rank_config(cfg_joined, rank, world, band)
 
     def loop(cfg, frames, cams=None):
@@ -503,7 +500,7 @@ def main():
             "data": f"reference scene {scene_name}.obj (Triangle[] from the reference loader, tests/golden/scenes), "
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
-                       "max_bounce": 10, "triangles": T, "row_band": band, "park": args.park,
+                       "max_bounce": 10, "triangles": T, "row_band": band,
                        "parallelism": (f"rows mod {world}" if band == 1 else
                                        f"bands of {band} rows mod {world} (row-tile split)")
                                       + "; each rank SDMA-copies its rows into the shared host frame"

@@ -87,11 +87,6 @@ typedef struct RtcRenderDesc {
                                       their places of the host frame (rtc_copy_rows_d2h_dma, its own PCIe link);
                                       without it the parts are gathered to device 0 over RCCL, re-interleaved there
                                       and copied once.  Same frame bit for bit. */
-#define RTC_F_PARK          0x2000 /* rtc_render_chain parks windows whose lanes bounce again after their first bounce
-                                      and runs their later bounces packed across windows (the default for scenes whose
-                                      bounce rays hit again, rtc_scene_upload's probe); RTC_F_NO_PARK never.  A/B timing
-                                      and tests; same frame bit for bit */
-#define RTC_F_NO_PARK       0x4000
 #define RTC_F_OVERLAP       0x800 /* frame pipelining (device-resident split only): the launch does not make
                                      `stream` wait for its sky pass, so the next launches on the same scene render
                                      (scratch in 8 slots) while this one's sky pass still runs.  A later overlapped

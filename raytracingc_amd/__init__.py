@@ -30,14 +30,11 @@ from ._abi import (  # noqa: F401
     RTC_F_NO_COOP,
     RTC_F_CHAIN_INLINE,
     RTC_F_OVERLAP,
-    RTC_F_PARK,
-    RTC_F_NO_PARK,
     RTC_F_HOST_ROWS,
     RTC_F_NO_REORDER,
     RTC_F_NO_TILE_CULL,
     RTC_SEGMENT_COUNTERS,
     RTC_EBUSY,
-    RTC_EINVAL,
     RTC_ETIMEDOUT,
     SCENE_DT,
     SPHERE_DT,
@@ -153,16 +150,13 @@ class RenderConfig:
     # frame pipelining (DeviceScene.render_rows_async): the launch does not join its sky pass into the stream;
     # the frame is complete at the scene's frame event (DeviceScene.set_frame_event); same frame
     overlap: bool = False
-    # rtc_render_chain's parking of windows that bounce again (RTC_F_PARK / RTC_F_NO_PARK): None = the scene's default
-    park: bool | None = None
 
     def flags(self) -> int:
         return ((RTC_F_HOIST_PRIMARY if self.hoist else 0) | (RTC_F_DEBUG_BOUNCES if self.debug_bounces else 0)
                 | (0 if self.tile_cull else RTC_F_NO_TILE_CULL) | (0 if self.reorder else RTC_F_NO_REORDER)
                 | (0 if self.coop else RTC_F_NO_COOP) | (0 if self.cluster_cull else RTC_F_NO_CLUSTER_CULL)
                 | (RTC_F_CHAIN_INLINE if self.chain_inline else 0) | (RTC_F_OVERLAP if self.overlap else 0)
-                | (RTC_F_HOST_ROWS if self.host_rows else 0)
-                | (0 if self.park is None else (RTC_F_PARK if self.park else RTC_F_NO_PARK)))
+                | (RTC_F_HOST_ROWS if self.host_rows else 0))
 
     def desc(self) -> RtcRenderDesc:
         return RtcRenderDesc(self.width, self.height, self.spp, self.max_bounce, int(self.triangles_only),

@@ -100,8 +100,6 @@ RTC_F_SPEC = 0x100
 RTC_F_PIPE = 0x200
 RTC_F_CHAIN_INLINE = 0x400
 RTC_F_OVERLAP = 0x800
-RTC_F_PARK = 0x2000
-RTC_F_NO_PARK = 0x4000
 RTC_F_HOST_ROWS = 0x1000
 RTC_SEGMENT_COUNTERS = 5  # u64 counters rtc_render_rows_async adds to (include/rtc.h)
 RTC_EINVAL, RTC_ENODEV, RTC_EIO, RTC_ENOMEM, RTC_EFORMAT = -10001, -10002, -10003, -10004, -10005

@@ -231,11 +231,6 @@ struct RtcDeviceScene {
      * geometry-pixel kernels are enqueued (before the join with the sky pass); null: none */
     hipEvent_t geoEvent;
     bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
-    /* rtc_render_chain's parking (kParkSlots windows per wave whose later bounces run packed): chosen at upload when the
-     * scene's bounce rays hit again (park), with its per-wave HBM slots grown on demand */
-    bool park;
-    void *parkBuf[kSkySlots + 1]; /* per overlap slot (two pipelined geometry kernels may run together), + joined */
-    size_t parkCap[kSkySlots + 1];
     bool timed;  /* the last launch was a split launch that recorded them */
 };
 
@@ -594,9 +589,6 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->segSlots);
     if (s->geoCounts)
         (void)hipFree(s->geoCounts);
-    for (void *b : s->parkBuf)
-        if (b)
-            (void)hipFree(b);
     if (s->evFork)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
@@ -667,7 +659,6 @@ struct RenderParams {
     int geoCap; /* entries per sub-list */
     int blocksX; /* 16x16 blocks per row of the launch */
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
-    float4 *__restrict__ parkBuf;       /* rtc_render_chain<.., PARK>: per wave kParkSlots x 4 x 64 float4 (see ParkMeta) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
     int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
     int chainPrimF;                 /* rtc_render_chain stages DevPrimF[triPadded] in LDS */
@@ -2542,121 +2533,10 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
 }
 
 /* COUNT: the launch asks for segment counters (instrumentation, untimed); without it the counters are compiled out */
-/* One iteration's shading of a window's lanes (calcColor, raytracing.c:272-293), after their closest hits c: the hit
- * branch (RandomDiretion's draws from the window's draw table, or from the lane's own state past it; emission, colour,
- * Russian roulette) or the miss branch (the environment).  rng: the lane's state at its window's index jn + lane; the
- * m-th hit of S_{jn + lane} draws at index jn + lane + m (see RTC_DRAW_TABLE).  nAct 0: no table (parked lanes). */
-template <bool COUNT>
-__device__ __forceinline__ void chain_shade(const RenderParams &P, const Closest &c, bool first, int iter, int nAct, int lane,
-                                            unsigned rng, V3 &pos, V3 &dir, V3 &rayColor, V3 &light, int &bounce,
-                                            unsigned &hits, bool &alive, unsigned &calls, ChainWaveLds &W,
-                                            const PowTablesLds &sPow)
-{
-#if RTC_DRAW_TABLE
-    /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
-    RngJump J{1u, 0u};
-    if (!first && __ballot(alive && c.idx >= 0 && lane + iter >= nAct))
-        J = rng_jump_by(7u * (unsigned)iter); /* wave-uniform */
-#endif
-    if (alive) {
-        if (COUNT)
-            calls++;
-        bool endSample;
-        if (c.idx >= 0) {
-            DSECT_BEGIN(dc2);
-            hits++;
-            /* calcColor hit branch, raytracing.c:272-287 */
-            const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
-            DevTri T;
-            DevMat M;
-            if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
-                const int u = __builtin_amdgcn_readfirstlane(c.idx);
-                T = KLOAD(KARG(tris), u);
-                M = KLOAD(KARG(mats), u);
-            } else {
-                T = P.tris[c.idx]; /* (kernel-argument pointers: global loads, not flat) */
-                M = P.mats[c.idx];
-            }
-            const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
-#if RTC_DRAW_TABLE
-            /* the hit draws (see RTC_DRAW_TABLE): the primary hit computes the lane's own and enters them in the table
-             * (every active lane hits there: one primary ray per wave); a later hit reads entry lane + iter, or computes
-             * it when that is past the window's active lanes */
-            float4 D;
-            if (first || lane + iter >= nAct) {
-                unsigned s = first ? rng : rng * J.a + J.c;
-                const V3 rd = random_direction(s);
-                D = make_float4(rd.x, rd.y, rd.z, random_value(s));
-                if (first)
-                    W.draw[lane] = D; /* read in later iterations, after chain_trace_pairs' LDS syncs */
-            } else {
-                D = W.draw[lane + iter];
-            }
-            const V3 diffuseDir = normalized(add(normal, V3{D.x, D.y, D.z}));
-#else
-            unsigned s = rng;
-            const V3 diffuseDir = normalized(add(normal, random_direction(s)));
-#endif
-            const V3 specularDir = reflect(dir, normal);
-            dir = lerp(diffuseDir, specularDir, M.smoothness);
-            pos = hitPoint;
-            const V3 emitted = mul(color, M.emission);
-            light = add(light, mulv(emitted, rayColor));
-            rayColor = mulv(rayColor, color);
-            const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-#if RTC_DRAW_TABLE
-            endSample = p < D.w;
-#else
-            endSample = p < random_value(s);
-#endif
-            if (!endSample) {
-                rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
-                bounce++;
-                endSample = bounce >= P.maxBounce;
-            }
-            DSECT_END(dc2, 2);
-        } else {
-            DSECT_BEGIN(dc6);
-#if defined(RTC_AB_CHEAP_ENV_CHAIN) && defined(RTC_EXPERIMENT) /* timing experiment only (the environment's cost) */
-            light = add(light, mulv(lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y, 0.f)), rayColor));
-#else
-            EnvParams env = KARG(env); /* the launch's sky and sun, the powf tables in LDS */
-            sPow.attach(env);
-            light = add(light, mulv(environment(dir, env), rayColor)); /* raytracing.c:291 */
-#endif
-            endSample = true;
-            DSECT_END(dc6, 6);
-        }
-        if (endSample)
-            alive = false;
-    }
-}
-
-/* PARK (scenes whose bounce rays hit again, e.g. fsuzane): a window whose lanes still bounce after their first bounce is
- * parked -- every lane's state to one of the wave's kParkSlots slots in HBM (RenderParams::parkBuf), the window's walk
- * deferred -- and the wave takes another item; once every slot holds a parked window (or no item is left) the parked
- * windows' later bounces run together, 64 continuing lanes to a pass (chain_drain in the kernel), and each parked window
- * is then walked as before.  Round 4's stamps: fsuzane's bounce iterations after the first took 45 % of the kernel's
- * wave-cycles at 9 % lane utilisation (about 6 live lanes of 64).  Same samples, same operations in the same order per
- * sample, same walk: the frame is unchanged. */
-constexpr int kParkSlots = 8;
-#ifndef RTC_PARK_MAX_CONT
-#define RTC_PARK_MAX_CONT 32
-#endif
-constexpr int kParkMaxCont = RTC_PARK_MAX_CONT; /* a window with more lanes that bounce again keeps them busy: not parked */
-struct ParkMeta { /* a parked (or ready) slot's item and window */
-    int it, code, k, nAct;
-    unsigned jn;
-    float acc[3];
-    unsigned long long cont; /* the window's lanes that still bounce */
-    unsigned long long m0, m1;
-};
-template <bool MULTI, bool COUNT, bool PARK = false> /* MULTI: more than one chunk of clusters (chunk-level culling, records from global) */
+template <bool MULTI, bool COUNT> /* MULTI: more than one chunk of clusters (chunk-level culling, records from global) */
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
-    static_assert(!PARK || (!MULTI && !COUNT), "parking: single-chunk scenes, untimed counters excluded");
-    __shared__ ParkMeta sPark[PARK ? kChainBlock / 64 : 1][PARK ? kParkSlots : 1];
     DSECT_BEGIN(dtot);
     DMARK_INIT(dcur);
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
@@ -2744,255 +2624,30 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     }
     if (lane == 0)
         nextIt = RTC_NEXT_ITEM();
-    /* PARK (wave-uniform): slots whose window waits for its later bounces (parked) and items waiting for their next
-     * window (ready) -- see ParkMeta */
-    unsigned parkedMask = 0, readyMask = 0;
-    const int waveIdx = threadIdx.x >> 6;
-    float4 *const parkBase = PARK ? P.parkBuf + ((size_t)blockIdx.x * (kChainBlock / 64) + waveIdx) * kParkSlots * 256 : nullptr;
-    constexpr unsigned kParkFull = (1u << kParkSlots) - 1u;
-    /* the samples of window slot S_{jn + lane} done: the walk through the window in sample order (main.c:99) */
-    const auto walk_window = [&](const V3 &light, unsigned hits, bool act, int nAct, int &k, unsigned &jn, float &acc,
-                                 int itw, bool deferred) {
-        const V3 t = mul(light, KARG(invSpp)); /* calcColor(...) * (float)(1./spp), main.c:99 */
-        const unsigned long long ones = __ballot(act && hits == 1u);
-        int p = 0;
-        SampleSlot *slot = P.sampleBuf + (size_t)itw * (size_t)P.spp;
-        /* in-kernel sums: the window's samples are staged in sample order in LDS -- the pair list's space, free
-         * until the next window's bounces; component c of staged sample i at stage[3 i + c] -- and lane c then adds
-         * them in order.  Interleaved, the three summing lanes read three consecutive dwords (three banks) and the
-         * staging lanes write at a stride of 3 dwords (a permutation of the 64 banks): no bank conflicts (round 4's
-         * stage[64 c + i] put the three readers on one bank: 6.3 M conflict cycles per 1080p launch) */
-        float *const stage = (float *)W.pair;
-        int staged = 0;
-        auto flush = [&]() {
-            wave_lds_sync();
-            if (lane < 3) {
-                const float *src = stage + lane;
-#pragma unroll 8
-                for (int i = 0; i < staged; ++i)
-                    acc = acc + src[3 * i];
-            }
-            wave_lds_sync();
-            staged = 0;
-        };
-        unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
-        while (k < P.spp && p < nAct) {
-            const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
-            const unsigned long long notOne = ~ones & win;
-            const int q = notOne ? __builtin_ctzll(notOne) : nAct;
-            const int take = min(q - p, P.spp - k);
-            /* a run of one-hit samples: j advances by 1 */
-            if (deferred) {
-#if !(defined(RTC_AB_NO_SLOTS) && defined(RTC_EXPERIMENT)) /* timing experiment only: nothing stored, no sum pass */
-                if (lane >= p && lane < p + take)
-                    slot[k + lane - p] = SampleSlot{t.x, t.y, t.z};
-#endif
-            } else {
-                if (lane >= p && lane < p + take) {
-                    const int i = 3 * (staged + lane - p);
-                    stage[i] = t.x;
-                    stage[i + 1] = t.y;
-                    stage[i + 2] = t.z;
-                }
-                staged += take;
-            }
-            mult += (lane >= p && lane < p + take) ? 1u : 0u;
-            k += take;
-            p += take;
-            if (k >= P.spp || p != q || q >= nAct)
-                break;
-            /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
-            const int hq = __builtin_amdgcn_readlane((int)hits, q);
-            const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q));
-            const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q));
-            const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q));
-            const int m = hq == 0 ? P.spp - k : 1; /* a primary miss: every remaining sample is this one */
-            if (deferred) {
-                for (int kk = k + lane; kk < k + m; kk += 64)
-                    slot[kk] = SampleSlot{qx, qy, qz};
-            } else if (m == 1) {
-                if (lane == q) {
-                    stage[3 * staged] = t.x;
-                    stage[3 * staged + 1] = t.y;
-                    stage[3 * staged + 2] = t.z;
-                }
-                ++staged;
-            } else { /* the staged samples first, then this one m times */
-                flush();
-                const float v = lane == 0 ? qx : (lane == 1 ? qy : qz);
-                for (int b2 = 0; b2 < m; ++b2)
-                    acc = acc + v;
-            }
-            mult += lane == q ? (unsigned)m : 0u;
-            k += m;
-            if (hq == 0)
-                break;
-            p = q + hq;
-        }
-        if (!deferred)
-            flush();
-        jn += (unsigned)p;
-        return mult;
-    };
-    /* the pixel's colour once its samples are accumulated (vec3ToColor, raytracing.c:11-15) */
-    const auto finish_item = [&](int itw, int code2, float acc, bool deferred) {
-        const int tile2 = code2 >> 6, bit2 = code2 & 63;
-        const int tX = KARG(blocksX) * 2;
-        const int x2 = (tile2 % tX) * 8 + (bit2 & 7), r2 = (tile2 / tX) * 8 + (bit2 >> 3);
-        if (deferred) {
-            if (lane == 0)
-                P.itemPix[itw] = r2 * KARG(width) + x2;
-        } else if (lane < 3) {
-            const size_t o = 3 * ((size_t)r2 * (size_t)KARG(width) + (size_t)x2) + (size_t)lane;
-            P.colors[o] = float_to_u8(acc);
-            if (P.accum)
-                P.accum[o] = acc;
-        }
-    };
-    /* PARK: the parked windows' later bounces, every continuing lane of every parked window packed 64 to a pass, all at
-     * the same bounce iteration (each window parked after its first bounce), then each parked window's walk in slot
-     * order: its item is done (pixel written, slot free) or waits for its next window (ready) */
-    const auto drain = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* the parked lanes' records, written by this wave */
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        ParkMeta *const pmeta = sPark[waveIdx];
-        int total = 0;
-        for (int q = 0; q < kParkSlots; ++q)
-            if ((parkedMask >> q) & 1u)
-                total += (int)__popcll(pmeta[q].cont);
-        for (int c0 = 0; c0 < total; c0 += 64) {
-            /* lane i: continuation c0 + i -- slot sp, lane lp of that slot's window (the n-th set bit of its mask) */
-            const int e = c0 + lane;
-            const bool valid = e < total;
-            int sp = 0, lp = 0, baseN = 0;
-            for (int q = 0; q < kParkSlots; ++q) {
-                if (!((parkedMask >> q) & 1u))
-                    continue;
-                unsigned long long m = pmeta[q].cont;
-                const int n = (int)__popcll(m);
-                if (valid && e >= baseN && e < baseN + n) {
-                    int want = e - baseN, pos2 = 0;
-#pragma unroll
-                    for (int wdt = 32; wdt >= 1; wdt >>= 1) {
-                        const int cnt = (int)__popcll(m & ((1ull << wdt) - 1ull));
-                        if (want >= cnt) {
-                            want -= cnt;
-                            m >>= wdt;
-                            pos2 += wdt;
-                        }
-                    }
-                    sp = q;
-                    lp = pos2;
-                }
-                baseN += n;
-            }
-            float4 *rec = parkBase + (size_t)sp * 256;
-            V3 pos{0.f, 0.f, 0.f}, dir{0.f, 0.f, 1.f}, rayColor{0.f, 0.f, 0.f}, light{0.f, 0.f, 0.f};
-            unsigned hits = 0, rngL = 0, calls = 0;
-            int bounce = 0;
-            bool alive = valid;
-            if (valid) {
-                const float4 q0 = rec[lp], q1 = rec[64 + lp], q2 = rec[128 + lp], q3 = rec[192 + lp];
-                light = V3{q0.x, q0.y, q0.z};
-                hits = __float_as_uint(q0.w);
-                pos = V3{q1.x, q1.y, q1.z};
-                bounce = __float_as_int(q1.w);
-                dir = V3{q2.x, q2.y, q2.z};
-                rngL = __float_as_uint(q2.w);
-                rayColor = V3{q3.x, q3.y, q3.z};
-            }
-            for (int iter = 2; __any(alive); ++iter) {
-#ifdef RTC_DIAG
-                dIters2++;
-                dAlive2 += (unsigned long long)__popcll(__ballot(alive));
-#endif
-                unsigned tt = 0;
-                const Closest c = chain_trace_pairs<MULTI, COUNT>(P, alive, false, pos, dir, sRec, W, lane, tt, sCl);
-                /* (nAct 0: every hit draws from its state, S_{jn + lane + iter}, as past a window's draw table) */
-                chain_shade<COUNT>(P, c, false, iter, 0, lane, rngL, pos, dir, rayColor, light, bounce, hits, alive, calls,
-                                   W, sPow);
-            }
-            if (valid)
-                rec[lp] = make_float4(light.x, light.y, light.z, __uint_as_float(hits));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (unsigned pmk = parkedMask; pmk; pmk &= pmk - 1u) {
-            const int sp = __builtin_ctz(pmk);
-            ParkMeta &pm = pmeta[sp];
-            const float4 q0 = parkBase[(size_t)sp * 256 + lane];
-            const int nAct = pm.nAct;
-            int k = pm.k;
-            unsigned jn = pm.jn;
-            float acc = lane < 3 ? pm.acc[lane] : 0.f;
-            const bool deferred = pm.it < P.sampleCap;
-            (void)walk_window(V3{q0.x, q0.y, q0.z}, __float_as_uint(q0.w), lane < nAct, nAct, k, jn, acc, pm.it, deferred);
-            if (k >= P.spp) {
-                finish_item(pm.it, pm.code, acc, deferred);
-            } else { /* its next window: a ready item */
-                if (lane == 0) {
-                    pm.k = k;
-                    pm.jn = jn;
-                }
-                if (lane < 3)
-                    pm.acc[lane] = acc;
-                readyMask |= 1u << sp;
-            }
-        }
-        parkedMask = 0u;
-        wave_lds_sync();
-    };
     DMARK(dcur, 19); /* prologue: staging, tables, the first item */
     for (;;) {
-        if constexpr (PARK) {
-            /* every slot holds a parked window, or no new item is left: the parked windows' later bounces, packed */
-            if (readyMask == 0 && parkedMask != 0 && (parkedMask == kParkFull || it >= nItems)) {
-                drain();
-                DMARK(dcur, 20);
-                continue;
-            }
-        }
-        int myIt, code, k = 0;
-        unsigned jn = 0;
-        float acc = 0.f; /* in-kernel sums (items without a deferred slot): the pixel's accumulator (main.c:97), component c in lane c */
-        unsigned long long m0, m1;
-        bool maskNext = true; /* the next new item's mask dwords requested (see the prefetch above) */
-        if (PARK && readyMask != 0u) { /* an item whose parked window has been walked: its next window */
-            const int sr = __builtin_ctz(readyMask);
-            readyMask &= readyMask - 1u;
-            const ParkMeta &pm = sPark[waveIdx][sr];
-            myIt = pm.it;
-            code = pm.code;
-            k = pm.k;
-            jn = pm.jn;
-            m0 = pm.m0;
-            m1 = pm.m1;
-            acc = lane < 3 ? pm.acc[lane] : 0.f;
-        } else {
-            if (it >= nItems)
-                break;
+        if (it >= nItems)
+            break;
 #if RTC_ITEM_PREFETCH
-            code = __builtin_amdgcn_readfirstlane((int)vc);
-            m0 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 0) |
-                 (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 1) << 32;
-            m1 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 2) |
-                 (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 3) << 32;
+        const int code = __builtin_amdgcn_readfirstlane((int)vc);
+        const unsigned long long m0 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 0) |
+                                      (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 1) << 32;
+        const unsigned long long m1 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 2) |
+                                      (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 3) << 32;
 #else /* round 4: scalar loads at the item's start */
-            code = __builtin_amdgcn_readfirstlane(KCONST(KARG(geoList))[entry_of(it)]);
-            const unsigned long long *mk = KARG(tileMask) + (size_t)(code >> 6) * P.maskWords;
-            m0 = KCONST(mk)[0], m1 = P.maskWords > 1 ? KCONST(mk)[1] : 0ull;
+        const int code = __builtin_amdgcn_readfirstlane(KCONST(KARG(geoList))[entry_of(it)]);
+        const unsigned long long *mk = KARG(tileMask) + (size_t)(code >> 6) * P.maskWords;
+        const unsigned long long m0 = KCONST(mk)[0], m1 = P.maskWords > 1 ? KCONST(mk)[1] : 0ull;
 #endif
-            /* the next item: its number (the LDS counter read at this item's previous start), its entry, and the counter
-             * for the one after */
-            const int itNext = __builtin_amdgcn_readfirstlane(nextIt);
-            if (RTC_ITEM_PREFETCH && itNext < nItems)
-                vc = gload(KARG(geoList), entry_of(itNext) + (size_t)vzero());
-            maskNext = !RTC_ITEM_PREFETCH || itNext >= nItems;
-            if (lane == 0)
-                nextIt = RTC_NEXT_ITEM();
-            myIt = it;
-            it = itNext;
-        }
+        /* the next item: its number (the LDS counter read at this item's previous start), its entry, and the counter for
+         * the one after */
+        const int itNext = __builtin_amdgcn_readfirstlane(nextIt);
+        if (RTC_ITEM_PREFETCH && itNext < nItems)
+            vc = gload(KARG(geoList), entry_of(itNext) + (size_t)vzero());
+        /* the next item's mask dwords requested (none needed past the end) */
+        bool maskNext = !RTC_ITEM_PREFETCH || itNext >= nItems;
+        if (lane == 0)
+            nextIt = RTC_NEXT_ITEM();
         const int tile = code >> 6, bit = code & 63;
         const int tilesX = KARG(blocksX) * 2;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
@@ -3000,9 +2655,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const int y = KARG(rowStart) + ((r >> sh) * KARG(rowStride) << sh) + (r & ((1 << sh) - 1));
         V3 pdir; /* main.c:88-94, as primary_dir */
         {
-            const int Wd = KARG(width), Hd = KARG(height);
-            const float dx = (float)(x - Wd / 2) / (float)(Hd / 2);
-            const float dy = (float)(y - Hd / 2) / (float)(Hd / 2);
+            const int W = KARG(width), H = KARG(height);
+            const float dx = (float)(x - W / 2) / (float)(H / 2);
+            const float dy = (float)(y - H / 2) / (float)(H / 2);
             pdir = normalized(add(add(mul(KARG(ex), dx), mul(KARG(ey), dy)), mul(KARG(ez), KARG(fov))));
         }
         const unsigned long long *mask = KARG(tileMask) + (size_t)tile * P.maskWords;
@@ -3011,7 +2666,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             for (int w = 0; w < P.maskWords; ++w)
                 L += (unsigned)__popcll(mask[w]);
         const unsigned seed = (unsigned)(x + y * KARG(width)); /* main.c:95 */
-        const bool deferred = myIt < P.sampleCap; /* wave-uniform */
+        const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
             closest_primary_listed_lds(pdir, prim, mask, m0, m1, sPF, pfStaged);
@@ -3021,7 +2676,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             }
         }
         DMARK(dcur, 15); /* item setup */
-        bool parkedItem = false;
+        /* in-kernel sums (items without a deferred slot): the pixel's accumulator (main.c:97), component c in lane c */
+        float acc = 0.f;
+        int k = 0;       /* samples accumulated */
+        unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
         while (k < P.spp && P.maxBounce > 0) {
             /* window: the state indices the remaining samples likely span (the pixel's hits per sample so far, a
              * margin; the first window assumes one hit per sample) */
@@ -3075,50 +2733,166 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     DMARK(dcur, bounce1 ? 17 : 20); /* bounce trace: the first bounce (17), later ones (20); 14 table, 3
                                                      * cull, 4 pair build, 5 pair passes inside */
                 }
-                chain_shade<COUNT>(P, c, first, iter, nAct, lane, rng, pos, dir, rayColor, light, bounce, hits, alive, calls,
-                                   W, sPow);
-                DMARK(dcur, iter < 2 ? 16 : 21); /* shading (2 hit, 6 environment inside); 21: after later bounces */
-                if constexpr (PARK) {
-                    /* after the first bounce: lanes still alive bounce again.  Park the window -- its lanes' state to
-                     * the wave's slot, its walk deferred -- and take other work; the parked windows' later bounces run
-                     * packed in chain_drain.  (With no free slot the window continues here.) */
-                    if (iter == 1) {
-                        const unsigned long long cont = __ballot(alive);
-                        const unsigned freeMask = ~(parkedMask | readyMask) & kParkFull;
-                        if (cont != 0ull && freeMask != 0u && __popcll(cont) <= kParkMaxCont) {
-                            const int sp = __builtin_ctz(freeMask);
-                            float4 *rec = parkBase + (size_t)sp * 256;
-                            rec[lane] = make_float4(light.x, light.y, light.z, __uint_as_float(hits));
-                            if (alive) { /* the ray state of the lanes that bounce again only */
-                                rec[64 + lane] = make_float4(pos.x, pos.y, pos.z, __int_as_float(bounce));
-                                rec[128 + lane] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(rng));
-                                rec[192 + lane] = make_float4(rayColor.x, rayColor.y, rayColor.z, 0.f);
-                            }
-                            ParkMeta &pm = sPark[waveIdx][sp];
-                            if (lane == 0) {
-                                pm.it = myIt;
-                                pm.code = code;
-                                pm.k = k;
-                                pm.nAct = nAct;
-                                pm.jn = jn;
-                                pm.cont = cont;
-                                pm.m0 = m0;
-                                pm.m1 = m1;
-                            }
-                            if (lane < 3)
-                                pm.acc[lane] = acc;
-                            parkedMask |= 1u << sp;
-                            parkedItem = true;
-                            break;
+#if RTC_DRAW_TABLE
+                /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
+                RngJump J{1u, 0u};
+                if (!first && __ballot(alive && c.idx >= 0 && lane + iter >= nAct))
+                    J = rng_jump_by(7u * (unsigned)iter); /* wave-uniform */
+#endif
+                if (alive) {
+                    if (counting)
+                        calls++;
+                    bool endSample;
+                    if (c.idx >= 0) {
+                        DSECT_BEGIN(dc2);
+                        hits++;
+                        /* calcColor hit branch, raytracing.c:272-287 */
+                        const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
+                        DevTri T;
+                        DevMat M;
+                        if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
+                            const int u = __builtin_amdgcn_readfirstlane(c.idx);
+                            T = KLOAD(KARG(tris), u);
+                            M = KLOAD(KARG(mats), u);
+                        } else {
+                            T = P.tris[c.idx]; /* (kernel-argument pointers: global loads, not flat) */
+                            M = P.mats[c.idx];
                         }
+                        const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
+#if RTC_DRAW_TABLE
+                        /* the hit draws (see RTC_DRAW_TABLE): the primary hit computes the lane's own and enters
+                         * them in the table (every active lane hits there: one primary ray per wave); a later hit
+                         * reads entry lane + iter, or computes it when that is past the window's active lanes */
+                        float4 D;
+                        if (first || lane + iter >= nAct) {
+                            unsigned s = first ? rng : rng * J.a + J.c;
+                            const V3 rd = random_direction(s);
+                            D = make_float4(rd.x, rd.y, rd.z, random_value(s));
+                            if (first)
+                                W.draw[lane] = D; /* read in later iterations, after chain_trace_pairs' LDS syncs */
+                        } else {
+                            D = W.draw[lane + iter];
+                        }
+                        const V3 diffuseDir = normalized(add(normal, V3{D.x, D.y, D.z}));
+#else
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+#endif
+                        const V3 specularDir = reflect(dir, normal);
+                        dir = lerp(diffuseDir, specularDir, M.smoothness);
+                        pos = hitPoint;
+                        const V3 emitted = mul(color, M.emission);
+                        light = add(light, mulv(emitted, rayColor));
+                        rayColor = mulv(rayColor, color);
+                        const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
+#if RTC_DRAW_TABLE
+                        endSample = p < D.w;
+#else
+                        endSample = p < random_value(rng);
+#endif
+                        if (!endSample) {
+                            rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
+                            bounce++;
+                            endSample = bounce >= P.maxBounce;
+                        }
+                        DSECT_END(dc2, 2);
+                    } else {
+                        DSECT_BEGIN(dc6);
+#ifdef RTC_AB_CHEAP_ENV_CHAIN /* timing experiment only (the environment's cost in the chain kernel) */
+                        light = add(light, mulv(lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y, 0.f)), rayColor));
+#else
+                        EnvParams env = KARG(env); /* the launch's sky and sun, the powf tables in LDS */
+                        sPow.attach(env);
+                        light = add(light, mulv(environment(dir, env), rayColor)); /* raytracing.c:291 */
+#endif
+                        endSample = true;
+                        DSECT_END(dc6, 6);
                     }
+                    if (endSample)
+                        alive = false;
                 }
+                DMARK(dcur, iter < 2 ? 16 : 21); /* shading (2 hit, 6 environment inside); 21: after later bounces */
             }
-            if (PARK && parkedItem)
-                break;
             (void)bounce;
             /* ---- walk the chain through the window, accumulating in sample order (main.c:99) ---- */
-            const unsigned mult = walk_window(light, hits, act, nAct, k, jn, acc, myIt, deferred);
+            const V3 t = mul(light, KARG(invSpp)); /* calcColor(...) * (float)(1./spp), main.c:99 */
+            const unsigned long long ones = __ballot(act && hits == 1u);
+            unsigned mult = 0; /* how many accumulated samples this lane's S_j is */
+            int p = 0;
+            SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
+            /* in-kernel sums: the window's samples are staged in sample order in LDS -- the pair list's space, free
+             * until the next window's bounces; component c of staged sample i at stage[3 i + c] -- and lane c then adds
+             * them in order.  Interleaved, the three summing lanes read three consecutive dwords (three banks) and the
+             * staging lanes write at a stride of 3 dwords (a permutation of the 64 banks): no bank conflicts (round 4's
+             * stage[64 c + i] put the three readers on one bank: 6.3 M conflict cycles per 1080p launch) */
+            float *const stage = (float *)W.pair;
+            int staged = 0;
+            auto flush = [&]() {
+                wave_lds_sync();
+                if (lane < 3) {
+                    const float *src = stage + lane;
+#pragma unroll 8
+                    for (int i = 0; i < staged; ++i)
+                        acc = acc + src[3 * i];
+                }
+                wave_lds_sync();
+                staged = 0;
+            };
+            while (k < P.spp && p < nAct) {
+                const unsigned long long win = (nAct >= 64 ? ~0ull : ((1ull << nAct) - 1ull)) & (~0ull << p);
+                const unsigned long long notOne = ~ones & win;
+                const int q = notOne ? __builtin_ctzll(notOne) : nAct;
+                const int take = min(q - p, P.spp - k);
+                /* a run of one-hit samples: j advances by 1 */
+                if (deferred) {
+#ifndef RTC_AB_NO_SLOTS /* timing experiment only (the deferred slots' cost): nothing stored, no sum pass */
+                    if (lane >= p && lane < p + take)
+                        slot[k + lane - p] = SampleSlot{t.x, t.y, t.z};
+#endif
+                } else {
+                    if (lane >= p && lane < p + take) {
+                        const int i = 3 * (staged + lane - p);
+                        stage[i] = t.x;
+                        stage[i + 1] = t.y;
+                        stage[i + 2] = t.z;
+                    }
+                    staged += take;
+                }
+                mult += (lane >= p && lane < p + take) ? 1u : 0u;
+                k += take;
+                p += take;
+                if (k >= P.spp || p != q || q >= nAct)
+                    break;
+                /* lane q: a sample with h != 1 (two or more hits, or none when the primary ray misses) */
+                const int hq = __builtin_amdgcn_readlane((int)hits, q);
+                const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.x), q));
+                const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.y), q));
+                const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.z), q));
+                const int m = hq == 0 ? P.spp - k : 1; /* a primary miss: every remaining sample is this one */
+                if (deferred) {
+                    for (int kk = k + lane; kk < k + m; kk += 64)
+                        slot[kk] = SampleSlot{qx, qy, qz};
+                } else if (m == 1) {
+                    if (lane == q) {
+                        stage[3 * staged] = t.x;
+                        stage[3 * staged + 1] = t.y;
+                        stage[3 * staged + 2] = t.z;
+                    }
+                    ++staged;
+                } else { /* the staged samples first, then this one m times */
+                    flush();
+                    const float v = lane == 0 ? qx : (lane == 1 ? qy : qz);
+                    for (int b = 0; b < m; ++b)
+                        acc = acc + v;
+                }
+                mult += lane == q ? (unsigned)m : 0u;
+                k += m;
+                if (hq == 0)
+                    break;
+                p = q + hq;
+            }
+            if (!deferred)
+                flush();
+            jn += (unsigned)p;
 #ifdef RTC_DIAG
             dWindows++;
             dAct += (unsigned)nAct;
@@ -3133,13 +2907,20 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 if (act && mult == 0)
                     segSpec += tests;
             }
-            (void)mult;
             DMARK(dcur, 7); /* walk and sums */
         }
-        if (!(PARK && parkedItem))
-            finish_item(myIt, code, acc, deferred);
+        if (deferred) {
+            if (lane == 0)
+                P.itemPix[it] = r * KARG(width) + x;
+        } else if (lane < 3) {
+            const size_t o = 3 * ((size_t)r * (size_t)KARG(width) + (size_t)x) + (size_t)lane;
+            P.colors[o] = float_to_u8(acc);
+            if (P.accum)
+                P.accum[o] = acc;
+        }
         if (!maskNext) /* (an item without a bounce iteration) */
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+        it = itNext;
         DMARK(dcur, 18); /* item tail: the pixel's colour */
     }
     DMARK(dcur, 15);
@@ -3252,8 +3033,6 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                         d->rowStart, d->rowStride);
     if ((long long)d->width * d->height > (1ll << 31) / 4)
         return rtc_fail(RTC_EINVAL, "frame too large");
-    if ((d->flags & RTC_F_PARK) && (d->flags & RTC_F_NO_PARK))
-        return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_PARK and RTC_F_NO_PARK together");
     if (d->flags & (RTC_F_COOP4 | RTC_F_COOP8 | RTC_F_PIPE | RTC_F_SPEC))
         return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: RTC_F_COOP4 / COOP8 / PIPE / SPEC name kernels that were "
                                     "removed (rtc_render_chain renders every geometry pixel)");
@@ -3566,26 +3345,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
             hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone[half] : nullptr;
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
-            /* parking (rtc_render_chain<.., PARK>): single-chunk scenes, timed launches, when the scene's bounce rays
-             * hit again (s->park, rtc_scene_upload's probe; RTC_F_PARK / RTC_F_NO_PARK override) */
-            const bool park = s->chunkCount <= 1 && !dSegments &&
-                              ((d->flags & RTC_F_PARK) || (s->park && !(d->flags & RTC_F_NO_PARK)));
-            if (park) {
-                const int region = overlap ? half : kSkySlots;
-                const size_t need = (size_t)cg.x * (kChainBlock / 64) * kParkSlots * 256 * sizeof(float4);
-                if (need > s->parkCap[region]) { /* hipFree waits for the device, so no kernel still reads it */
-                    if (ms->parkBuf[region])
-                        HIP_TRY(hipFree(ms->parkBuf[region]));
-                    ms->parkBuf[region] = nullptr;
-                    ms->parkCap[region] = 0;
-                    HIP_TRY(hipMalloc(&ms->parkBuf[region], need));
-                    ms->parkCap[region] = need;
-                }
-                P.parkBuf = (float4 *)s->parkBuf[region];
-            }
-            if (park)
-                HIP_TRY(launch_stop(rtc_render_chain<false, false, true>, cg, cb, dyn, gs, chainStop, P));
-            else if (s->chunkCount > 1 && dSegments)
+            if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, gs, chainStop, P));
             else if (s->chunkCount > 1)
                 HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, dyn, gs, chainStop, P));

@@ -413,54 +413,6 @@ def test_overlapped_frames_bit_exact(variant, size, gpu_available):
     ds.close()
 
 
-@pytest.mark.parametrize("scene_name,size", [("fsuzane", (160, 90, 64)), ("fsuzane", (1920, 1080, 8)),
-                                             ("complex", (320, 180, 16)), ("ultracomplex", (256, 144, 32)),
-                                             ("cube", (200, 120, 16)), ("fsuzane", (33, 17, 3))])
-@pytest.mark.parametrize("overlap", [False, True])
-def test_parked_windows_bit_exact(scene_name, size, overlap, gpu_available):
-    """RTC_F_PARK: windows whose lanes bounce again after their first bounce are parked in HBM and their later bounces
-    run packed across parked windows (rtc_render_chain<.., PARK>).  Joined launches (deferred sample slots at 1080p,
-    in-kernel sums below) and pipelined ones (in-kernel sums), several cameras: colours AND the float accumulators
-    equal rtc_render's (no parking) bit for bit; RTC_F_NO_PARK likewise."""
-    import torch
-
-    tris, _ = load_tris(scene_name)
-    scene = rt.default_scene()
-    cams = [rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1)]
-    W, H, spp = size
-    base = rt.RenderConfig(W, H, spp, 10, True)
-    refs = [rt.render(tris, None, scene, c, base, want_accum=True) for c in cams]
-    ds = rt.DeviceScene(tris, None)
-    st = torch.cuda.Stream()
-    for park in (True, False):
-        cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=overlap, park=park)
-        for c, (rc, ra, _) in zip(cams, refs):
-            buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-            acc = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
-            ds.render_rows_async(scene, c, cfg, buf.data_ptr(), accum_ptr=acc.data_ptr(), stream=st.cuda_stream)
-            torch.cuda.synchronize()
-            assert np.array_equal(buf.cpu().numpy(), rc), (park, c)
-            assert np.array_equal(acc.cpu().numpy().view(np.uint32), ra.view(np.uint32)), (park, c)
-    ds.close()
-
-
-def test_park_flags_conflict(gpu_available):
-    """RTC_F_PARK together with RTC_F_NO_PARK is RTC_EINVAL."""
-    import ctypes as C
-
-    import torch
-
-    tris, _ = load_tris("fsuzane")
-    ds = rt.DeviceScene(tris, None)
-    d = rt.RenderConfig(64, 32, 4, 10, True, park=True).desc()
-    d.flags |= rt.RTC_F_NO_PARK
-    buf = torch.zeros((32, 64, 3), dtype=torch.uint8, device="cuda")
-    rc = rt.lib().rtc_render_rows_async(ds._h, C.byref(rt.default_scene()), C.byref(rt.camera_basis()), C.byref(d),
-                                        C.c_void_p(buf.data_ptr()), None, None, None)
-    assert rc == rt.RTC_EINVAL
-    ds.close()
-
-
 def test_overlap_slot_ring(gpu_available):
     """RTC_F_OVERLAP launches cycle through 8 scratch slots and wait for the unjoined sky passes only when one reads
     the slot being rewritten or writes the same buffer with another camera: 20 back-to-back frames of one camera

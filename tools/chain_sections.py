@@ -34,8 +34,7 @@ for hoist in (False, True):
     # pipelined launches like the bench's timed frames (in-kernel sums on the alternating streams), one at a time
     import torch
 
-    park = {"": None, "1": True, "0": False}[os.environ.get("RTC_SECT_PARK", "")]
-    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, overlap=True, park=park)
+    cfg = rt.RenderConfig(W, H, SPP, 10, True, hoist=hoist, overlap=True)
     ds = rt.DeviceScene(tris, None)
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
     st = torch.cuda.Stream()
