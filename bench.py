@@ -340,6 +340,7 @@ def main():
     nbuf = 3
     # this rank's compact rows of each frame in HBM; the host frames: pinned (N = 1) or node-shared (N > 1)
     dev_rows = [torch.zeros((rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    torch.cuda.synchronize(dev)  # (the zero fills ran on the current stream; the frames render on `stream`)
     shared = None
     if multi:
         shared = SharedHostFrames(f"rtc_bench_{os.environ.get('MASTER_PORT', '0')}", nbuf, H, W, local, barrier)

@@ -378,6 +378,7 @@ def test_overlapped_frames_bit_exact(variant, size, gpu_available):
     st, cp = torch.cuda.Stream(), torch.cuda.Stream()
     nb = 2
     bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     freed = [None] * nb
     got = []
     def new_event():  # a torch event has no hipEvent_t until its first record
@@ -429,6 +430,7 @@ def test_overlap_slot_ring(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     for _ in range(20):
         ds.render_rows_async(scene, cams[1], cfg, buf.data_ptr(), stream=st.cuda_stream)
     torch.cuda.synchronize()
@@ -632,6 +634,7 @@ def test_overlapped_then_other_launches_same_buffer(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     for follow in ({}, {"tile_cull": False}, {"coop": False}, {"debug_bounces": True}, {"hoist": True}):
         cfg_b = rt.RenderConfig(W, H, spp, 10, True, **follow)
         ref_b, _, _ = rt.render(tris, None, scene, cam_b, cfg_b)
@@ -657,6 +660,7 @@ def test_frame_event_is_one_shot(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     for overlap in (True, False):
         cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=overlap)
         ev, geo = torch.cuda.Event(), torch.cuda.Event()
@@ -846,6 +850,7 @@ def test_frame_loop_pipelined_host_frames(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     dev = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(3)]
     out = ds.frame_loop(scene, cam, rt.RenderConfig(W, H, spp, 10, True), [d.data_ptr() for d in dev],
                         [h.data_ptr() for h in host], W * 3, 7, st.cuda_stream)
@@ -919,6 +924,7 @@ def test_4k_row_shares_assemble_bit_exact(scene, spp, G, band, gpu_available):
     host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     dev = [torch.zeros((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     lst = torch.cuda.Stream()
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     for r in range(G):
         cfg = rank_config(full, r, G, band)
         ds.frame_loop(sc, cam, cfg, [d.data_ptr() for d in dev], [h.data_ptr() + r * band * W * 3 for h in host],
@@ -955,6 +961,7 @@ def test_prep_skip_across_streams(gpu_available):
         for s, c, want in ((sa, cam, ref), (sb, cam, ref), (sa, cam, ref), (sa, cam, ref), (sa, cam2, ref2),
                            (sb, cam2, ref2), (sa, cam, ref)):
             buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
             ev = torch.cuda.Event()
             ev.record(s)
             ds.set_frame_event(ev.cuda_event)
@@ -979,6 +986,7 @@ def test_moving_camera_frame_loop(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     dev = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     host = [torch.zeros((H, W, 3), dtype=torch.uint8, pin_memory=True) for _ in range(3)]
     out = ds.frame_loop(scene, cams, rt.RenderConfig(W, H, spp, 10, True), [d.data_ptr() for d in dev],
                         [h.data_ptr() for h in host], W * 3, frames, st.cuda_stream)
@@ -1001,6 +1009,7 @@ def test_empty_launch_consumes_frame_event(gpu_available):
     ds = rt.DeviceScene(tris, None)
     st = torch.cuda.Stream()
     buf = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # (the zero fills ran on the current stream, not the launch stream)
     ev = torch.cuda.Event()
     ev.record(st)
     ds.set_frame_event(ev.cuda_event)
