@@ -1368,7 +1368,10 @@ __device__ bool tile_prunes(const TileCone &K, const DevPrimF &F)
 #define RTC_CULL_SUPER 1
 #endif
 constexpr int kSuperBlocks = 4;
-constexpr size_t kSuperCullPixels = 400000; /* launches of more pixels run level 0 */
+#ifndef RTC_SUPER_CULL_PIXELS
+#define RTC_SUPER_CULL_PIXELS 400000
+#endif
+constexpr size_t kSuperCullPixels = RTC_SUPER_CULL_PIXELS; /* launches of more pixels run level 0 */
 __global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned long long *__restrict__ superMask)
 {
     const int sx = blockIdx.x, sy = blockIdx.y, lane = threadIdx.x;
