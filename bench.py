@@ -501,7 +501,7 @@ def main():
             "data": f"reference scene {scene_name}.obj (Triangle[] from the reference loader, tests/golden/scenes), "
                     "default camera/sky/sun, per-pixel seed x+y*W",
             "config": {"workload": args.workload, "scene": f"{scene_name}.obj", "width": W, "height": H, "spp": spp,
-                       "max_bounce": 10, "triangles": T, "row_band": band,
+                       "max_bounce": 10, "triangles": T, "row_band": band, "chain_wgs_per_cu": ds.chain_wgs,
                        "parallelism": (f"rows mod {world}" if band == 1 else
                                        f"bands of {band} rows mod {world} (row-tile split)")
                                       + "; each rank SDMA-copies its rows into the shared host frame"

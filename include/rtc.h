@@ -208,6 +208,12 @@ int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event);
  * (rtc_render_rows_async returned). */
 int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event);
 int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2]);
+/* Scheduling hints chosen at upload (no reference counterpart; they never change a frame):
+ * rtc_bounce_hit_share estimates (host only, fixed-seed probe) the share of diffuse bounce rays from the triangles that
+ * hit the scene again; rtc_scene_chain_wgs reports the geometry kernel's workgroups per CU for whole frames that the
+ * scene got from it (4 above 0.15, else 3; small row shares run 3). */
+int rtc_bounce_hit_share(const Triangle *tris, int triCount, float *share);
+int rtc_scene_chain_wgs(const RtcDeviceScene *s);
 int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                           const RtcRenderDesc *d, void *dColors, float *dAccum,
                           unsigned long long *dSegments, void *stream);

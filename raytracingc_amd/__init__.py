@@ -35,6 +35,7 @@ from ._abi import (  # noqa: F401
     RTC_F_NO_TILE_CULL,
     RTC_SEGMENT_COUNTERS,
     RTC_EBUSY,
+    RTC_EINVAL,
     RTC_ETIMEDOUT,
     SCENE_DT,
     SPHERE_DT,
@@ -231,6 +232,11 @@ class DeviceScene:
                                           C.c_void_p(segments_ptr) if segments_ptr else None,
                                           C.c_void_p(stream) if stream else None), "rtc_render_rows_async")
 
+    @property
+    def chain_wgs(self) -> int:
+        """rtc_render_chain's workgroups per CU for whole frames, chosen at upload (rtc_scene_chain_wgs)."""
+        return lib().rtc_scene_chain_wgs(self._h)
+
     def set_timing(self, enable: bool):
         """Record HIP events around the split launch's kernels from now on (rtc_scene_set_timing)."""
         check(lib().rtc_scene_set_timing(self._h, int(enable)), "rtc_scene_set_timing")
@@ -342,6 +348,15 @@ def deinterleave_async(compact_ptr: int, parts: int, rows_per_part: int, width: 
     check(lib().rtc_deinterleave_async(C.c_void_p(compact_ptr), parts, rows_per_part, width, height,
                                        C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None),
           "rtc_deinterleave_async")
+
+
+def bounce_hit_share(tris) -> float:
+    """rtc_bounce_hit_share: the share of diffuse bounce rays from the triangles that hit the scene again (host probe,
+    a scheduling hint)."""
+    t, nt = _arr(tris, TRIANGLE_DT)
+    out = C.c_float()
+    check(lib().rtc_bounce_hit_share(_ptr(t), nt, C.byref(out)), "rtc_bounce_hit_share")
+    return out.value
 
 
 def vec3ToColor(accum: np.ndarray) -> np.ndarray:

@@ -136,6 +136,7 @@ EXPORTS = [
     "rtc_scene_set_sun", "rtc_camera_basis", "rtc_write_bmp", "rtc_quantize",
     "rtc_render", "rtc_render_multi",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
+    "rtc_bounce_hit_share", "rtc_scene_chain_wgs",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
     "rtc_deinterleave_async", "rtc_deinterleave_bands_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
     "rtc_host_unregister", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
@@ -188,6 +189,8 @@ def lib() -> C.CDLL:
     L.rtc_scene_upload.argtypes = [vp, ip, vp, ip, ip, C.POINTER(vp)]
     L.rtc_scene_release.argtypes = [vp]
     L.rtc_scene_kernel_times.argtypes = [vp, vp]
+    L.rtc_bounce_hit_share.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
+    L.rtc_scene_chain_wgs.argtypes = [vp]
     L.rtc_scene_set_timing.argtypes = [vp, C.c_int]
     L.rtc_scene_set_geometry_event.argtypes = [vp, vp]
     L.rtc_scene_set_frame_event.argtypes = [vp, vp]

@@ -155,6 +155,16 @@ struct __attribute__((aligned(32))) DevCluster {
 constexpr unsigned kOrderEventFlags = hipEventDisableTiming | (RTC_ORDER_FENCE ? 0u : hipEventDisableSystemFence);
 /* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
 constexpr int kSkySlots = 8;
+#ifndef RTC_CHAIN_WGS_FULL
+#define RTC_CHAIN_WGS_FULL 3
+#endif
+#ifndef RTC_CHAIN_WGS_HIT
+#define RTC_CHAIN_WGS_HIT 4 /* whole frames of scenes whose bounce-hit share (bounce_hit_share) exceeds RTC_WGS_HIT_SHARE */
+#endif
+#ifndef RTC_WGS_HIT_SHARE
+#define RTC_WGS_HIT_SHARE 0.15
+#endif
+
 /* rtc_render_chain's geometry-pixel sub-lists: kGeoLists counters, kGeoCountStride ints (one 128-B line) apart; a ring
  * of kGeoRing counter sets of kGeoSetInts ints (see RtcDeviceScene::geoCounts) */
 constexpr int kGeoLists = 16, kGeoCountStride = 32;
@@ -198,6 +208,8 @@ struct RtcDeviceScene {
     unsigned long long geoSeq;
     hipStream_t cullStream;
     bool cullValid;
+    double hitShare;  /* bounce_hit_share at upload */
+    int chainWgsFull; /* rtc_render_chain workgroups per CU for whole frames */
     /* rtc_prep_primary's records of slot h are for prepOrigin[h], written on prepStream[h] (prepValid[h]: they exist) */
     bool prepValid[kSkySlots];
     float prepOrigin[kSkySlots][3];
@@ -233,6 +245,89 @@ struct RtcDeviceScene {
     bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
     bool timed;  /* the last launch was a split launch that recorded them */
 };
+
+/* The share of diffuse bounce rays that hit the scene again, estimated at upload (host, a fixed-seed probe): rays from
+ * area-weighted random points of the triangles, in directions normal + a random unit vector (the reference's diffuse
+ * lobe, raytracing.c:276-279, without the specular part), tested against every triangle in double precision with the
+ * reference's backface rule.  Only a scheduling hint (rtc_render_chain's workgroups per CU): it never changes a
+ * frame.  Measured shares: fsuzane 0.21, rsuzanne 0.11, ultracomplex 0.019, complex 0.016, cube 0. */
+static double bounce_hit_share(const Triangle *t, int n)
+{
+    if (n <= 0)
+        return 0.0;
+    struct D3 { double x, y, z; };
+    const auto sub3 = [](D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; };
+    const auto dot3 = [](D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
+    const auto cross3 = [](D3 a, D3 b) { return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; };
+    const auto d3 = [](vec3 v) { return D3{v.x, v.y, v.z}; };
+    std::vector<double> cdf((size_t)n);
+    double total = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const D3 c = cross3(sub3(d3(t[i].posB), d3(t[i].posA)), sub3(d3(t[i].posC), d3(t[i].posA)));
+        total += 0.5 * std::sqrt(dot3(c, c));
+        cdf[(size_t)i] = total;
+    }
+    if (!(total > 0.0))
+        return 0.0;
+    unsigned long long st = 0x9E3779B97F4A7C15ull;
+    const auto uni = [&]() { /* xorshift64*, [0, 1) */
+        st ^= st >> 12;
+        st ^= st << 25;
+        st ^= st >> 27;
+        return (double)((st * 0x2545F4914F6CDD1Dull) >> 11) * (1.0 / 9007199254740992.0);
+    };
+    const int rays = (int)std::min<long long>(2048, std::max<long long>(256, 4000000LL / n));
+    int hits = 0;
+    for (int r = 0; r < rays; ++r) {
+        const int i = (int)(std::lower_bound(cdf.begin(), cdf.end(), uni() * total) - cdf.begin());
+        const Triangle &T = t[std::min(i, n - 1)];
+        double u = uni(), w = uni();
+        if (u + w > 1.0) {
+            u = 1.0 - u;
+            w = 1.0 - w;
+        }
+        const D3 A = d3(T.posA), AB = sub3(d3(T.posB), A), AC = sub3(d3(T.posC), A);
+        D3 nn = d3(T.normal);
+        const double nl = std::sqrt(dot3(nn, nn));
+        if (!(nl > 0.0))
+            continue;
+        nn = D3{nn.x / nl, nn.y / nl, nn.z / nl};
+        D3 q{0, 0, 0};
+        double ql = 0.0;
+        do { /* a uniform random unit vector (rejection from the cube) */
+            q = D3{2 * uni() - 1, 2 * uni() - 1, 2 * uni() - 1};
+            ql = dot3(q, q);
+        } while (ql > 1.0 || ql < 1e-12);
+        ql = std::sqrt(ql);
+        D3 dir{nn.x + q.x / ql, nn.y + q.y / ql, nn.z + q.z / ql};
+        const double dl = std::sqrt(dot3(dir, dir));
+        if (!(dl > 1e-9))
+            continue;
+        dir = D3{dir.x / dl, dir.y / dl, dir.z / dl};
+        const D3 P{A.x + u * AB.x + w * AC.x + 1e-4 * nn.x, A.y + u * AB.y + w * AC.y + 1e-4 * nn.y,
+                   A.z + u * AB.z + w * AC.z + 1e-4 * nn.z};
+        for (int j = 0; j < n; ++j) { /* rayTriangle's tests (raytracing.c:186-214), in double */
+            if (dot3(dir, d3(t[j].normal)) >= 0.0)
+                continue;
+            const D3 a = d3(t[j].posA), ab = sub3(d3(t[j].posB), a), ac = sub3(d3(t[j].posC), a);
+            const D3 h = cross3(dir, ac);
+            const double det = dot3(ab, h);
+            if (std::fabs(det) < 1e-12)
+                continue;
+            const D3 sv = sub3(P, a);
+            const double uu = dot3(sv, h) / det;
+            if (uu < 0.0 || uu > 1.0)
+                continue;
+            const D3 qv = cross3(sv, ab);
+            const double vv = dot3(dir, qv) / det;
+            if (vv < 0.0 || uu + vv > 1.0 || dot3(ac, qv) / det < 1e-3)
+                continue;
+            ++hits;
+            break;
+        }
+    }
+    return (double)hits / (double)rays;
+}
 
 static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
                        std::vector<DevMat> &dm, std::vector<DevSphere> &ds)
@@ -448,6 +543,21 @@ static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std:
     }
 }
 
+extern "C" int rtc_bounce_hit_share(const Triangle *tris, int triCount, float *share)
+{
+    if (!share || triCount < 0 || (triCount > 0 && !tris))
+        return rtc_fail(RTC_EINVAL, "rtc_bounce_hit_share: bad argument");
+    *share = (float)bounce_hit_share(tris, triCount);
+    return 0;
+}
+
+extern "C" int rtc_scene_chain_wgs(const RtcDeviceScene *s)
+{
+    if (!s)
+        return rtc_fail(RTC_EINVAL, "rtc_scene_chain_wgs: null scene");
+    return s->chainWgsFull;
+}
+
 extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount, int device,
                                 RtcDeviceScene **out)
 {
@@ -486,6 +596,12 @@ extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere
     s->maskWords = (s->triPadded + 63) / 64;
     s->clusterCount = (triCount + kClusterSize - 1) / kClusterSize;
     s->chunkCount = (s->clusterCount + kChunkClusters - 1) / kChunkClusters;
+    /* whole frames of scenes whose bounce rays often hit again (fsuzane) run 4 chain workgroups per CU: their frame is
+     * nearly all geometry kernel, which then has the registers the co-resident sky waves would use (round 5, 1080p x64:
+     * fsuzane 1.25 -> 1.16 ms per frame; ultracomplex 0.348 -> 0.379, complex 4K 1.22 -> 1.34, so 3 stays the default,
+     * profiles/r05_w4_ab_chain_wgs.log) */
+    s->hitShare = bounce_hit_share(tris, triCount);
+    s->chainWgsFull = s->hitShare > RTC_WGS_HIT_SHARE ? RTC_CHAIN_WGS_HIT : RTC_CHAIN_WGS_FULL;
     hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
     if (e == hipSuccess)
         e = hipMalloc(&s->clTris, ct.size() * sizeof(DevTri));
@@ -2076,11 +2192,9 @@ constexpr int kChainBlock = RTC_CHAIN_BLOCK; /* threads per chain workgroup */
  * in the chain kernel's idle issue slots instead of waiting for its tail, and the launch stream's small kernels are no
  * longer starved by that tail (round 4: frame 0.372 -> 0.351 ms; 4 per CU: 0.370 vs 0.340 ms on the alternating streams,
  * though fsuzane, whose frame is nearly all geometry kernel, takes 1.12 vs 1.22 ms with 4).  Small shares run 3 too since
- * consecutive shares overlap on the alternating streams (4 before).  Workers = per-CU count x CUs: exactly the resident
- * capacity, no second round. */
-#ifndef RTC_CHAIN_WGS_FULL
-#define RTC_CHAIN_WGS_FULL 3
-#endif
+ * consecutive shares overlap on the alternating streams (4 before).  Round 5: whole frames of scenes whose bounce rays
+ * often hit again run 4 (RTC_CHAIN_WGS_HIT, chosen at upload by bounce_hit_share).  Workers = per-CU count x CUs:
+ * exactly the resident capacity, no second round.  (RTC_CHAIN_WGS_FULL / _HIT are defined with kSkySlots.) */
 #ifndef RTC_CHAIN_WGS_SHARE
 #define RTC_CHAIN_WGS_SHARE 3 /* 1/4 share 0.116 -> 0.113 ms, 1/8 share 0.075 -> 0.074 ms (round 4, r04_za) */
 #endif
@@ -3337,7 +3451,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evHeavy0, gs));
             /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
              * filter records when the block stays within 4 per CU */
-            const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : RTC_CHAIN_WGS_FULL;
+            const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : s->chainWgsFull;
             const size_t rec = s->chunkCount <= 1 ? (size_t)soa_slots(s->clusterCount * kClusterSize) * sizeof(DevTri) : 0;
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
             P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;

@@ -199,6 +199,17 @@ def test_tile_cull_many_triangles(gpu_available):
     assert over == 0 and s1["segments"] == oseg
 
 
+def test_chain_occupancy_hint(gpu_available):
+    """rtc_scene_chain_wgs: whole frames of scenes whose bounce rays often hit again (bounce_hit_share > 0.15: fsuzane)
+    run 4 geometry-kernel workgroups per CU, the others 3; the frame is the same either way (fsuzane's
+    full-size frame: test_full_size_baseline_configs)."""
+    for name, want in (("fsuzane", 4), ("ultracomplex", 3), ("complex", 3), ("cube", 3)):
+        tris, _ = load_tris(name)
+        ds = rt.DeviceScene(tris, None)
+        assert ds.chain_wgs == want, name
+        ds.close()
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_random_configurations_match_oracle(seed, gpu_available):
     """Randomised end-to-end parity against the CPU restatement (the oracle pinned to the reference's fixtures):

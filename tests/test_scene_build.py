@@ -175,3 +175,20 @@ def test_obj_export_round_trip(name, tmp_path):
     assert rt.loadOBJTriangles(obj).tobytes() == want.tobytes()
     if have_ref_binary():
         assert _ref_dump(obj, str(tmp_path)).tobytes() == want.tobytes()
+
+
+def test_bounce_hit_share_probe():
+    """rtc_bounce_hit_share (host only): the upload-time probe behind the geometry kernel's workgroups per CU -- a
+    scheduling hint, never a change of frame.  Deterministic; the scenes whose bounces hit again (fsuzane) above the
+    0.15 threshold, the convex-ish BASELINE scenes well below it; no triangles -> 0; bad arguments refused."""
+    import ctypes as C
+
+    shares = {}
+    for name in ("fsuzane", "ultracomplex", "complex", "cube"):
+        tris, _ = load_tris(name)
+        shares[name] = rt.bounce_hit_share(tris)
+        assert rt.bounce_hit_share(tris) == shares[name]
+    assert shares["fsuzane"] > 0.15
+    assert max(shares["ultracomplex"], shares["complex"], shares["cube"]) < 0.05
+    assert rt.bounce_hit_share(None) == 0.0
+    assert rt.lib().rtc_bounce_hit_share(None, 3, C.byref(C.c_float())) == rt.RTC_EINVAL
