@@ -1297,6 +1297,25 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
 constexpr int kDiagSects = 24;
 __device__ unsigned long long g_rtc_sect[kDiagSects]; /* [8..12] window statistics (rtc_render_chain) */
+/* rtc_render_chain's waves: (start, end, items) by s_memrealtime (the 100 MHz constant clock, the same on every
+ * CU), one record per wave of the last launches until the log is full (rtc_diag_wavelog) */
+constexpr int kWaveLog = 16384;
+__device__ unsigned long long g_rtc_wavelog[kWaveLog][3];
+__device__ unsigned g_rtc_wavecount;
+extern "C" int rtc_diag_wavelog(unsigned long long *out, int maxWaves, int reset)
+{
+    unsigned n = 0;
+    HIP_TRY(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rtc_wavecount), sizeof n));
+    n = std::min<unsigned>(n, (unsigned)kWaveLog);
+    if (out && maxWaves > 0)
+        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_wavelog),
+                                    std::min<unsigned>(n, (unsigned)maxWaves) * 3 * sizeof(unsigned long long)));
+    if (reset) {
+        const unsigned z = 0;
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_wavecount), &z, sizeof z));
+    }
+    return (int)n;
+}
 #define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 /* per-block records of rtc_tile_cull (wave 0): {start, level 1 done, end, geometry, level-2 prefilter cycles, candidate
  * loop cycles, candidates, 0}, written with plain stores into the buffer rtc_diag_set_cull_buffer names (null: none) */
@@ -2656,6 +2675,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 {
     DSECT_BEGIN(dtot);
     DMARK_INIT(dcur);
+#ifdef RTC_DIAG
+    const unsigned long long dWaveT0 = __builtin_amdgcn_s_memrealtime();
+    unsigned dWaveItems = 0;
+#endif
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
@@ -3038,6 +3061,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         if (!maskNext) /* (an item without a bounce iteration) */
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
         it = itNext;
+#ifdef RTC_DIAG
+        dWaveItems++;
+#endif
         DMARK(dcur, 18); /* item tail: the pixel's colour */
     }
     DMARK(dcur, 15);
@@ -3059,6 +3085,16 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     if (counting)
         flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
+#ifdef RTC_DIAG
+    if (lane == 0) {
+        const unsigned w = atomicAdd(&g_rtc_wavecount, 1u);
+        if (w < (unsigned)kWaveLog) {
+            g_rtc_wavelog[w][0] = dWaveT0;
+            g_rtc_wavelog[w][1] = __builtin_amdgcn_s_memrealtime();
+            g_rtc_wavelog[w][2] = dWaveItems;
+        }
+    }
+#endif
 }
 
 /* A kernel launch whose completion also records `stop` (null: a plain launch): the event is the dispatch's own
