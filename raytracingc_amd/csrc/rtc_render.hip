@@ -2219,7 +2219,7 @@ constexpr int kChainBlock = RTC_CHAIN_BLOCK; /* threads per chain workgroup */
 #define RTC_CHAIN_WGS_SHARE 3 /* 1/4 share 0.116 -> 0.113 ms, 1/8 share 0.075 -> 0.074 ms (round 4, r04_za) */
 #endif
 #ifndef RTC_CHAIN_UNROLL
-#define RTC_CHAIN_UNROLL 2
+#define RTC_CHAIN_UNROLL 4 /* the pair passes' record loop (round 5: 4 vs 2, fsuzane -1 %, headline within noise; same registers) */
 #endif
 #ifndef RTC_CHAIN_WAVES
 #define RTC_CHAIN_WAVES 4
