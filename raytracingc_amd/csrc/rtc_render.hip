@@ -158,6 +158,21 @@ constexpr int kSkySlots = 8;
 #ifndef RTC_CHAIN_WGS_FULL
 #define RTC_CHAIN_WGS_FULL 3
 #endif
+#ifndef RTC_CULL_PRIO
+#define RTC_CULL_PRIO 0
+#endif
+/* Wave priority of the geometry kernel (s_setprio): its waves are issued before the sky pass's on a shared SIMD.  A row
+ * share's chain kernel runs ~3 pixels per wave; as its waves retire, sky waves fill their slots and the remaining chain
+ * waves -- the share's critical path -- got a sixth of the issue: a wave's third and fourth pixels took 2-7x its first
+ * (tools/wave_spread.py).  Round 5: 1080p 1/8 share 0.0757 -> 0.0697 ms, whole frames unchanged (the sky pass still
+ * fills the chain kernel's idle slots); the tile cull at priority 3 too (RTC_CULL_PRIO) within noise of it
+ * (profiles/r05_pr_ab_wave_priority.log) */
+#ifndef RTC_CHAIN_PRIO
+#define RTC_CHAIN_PRIO 3
+#endif
+#ifndef RTC_GEO_CLASSES
+#define RTC_GEO_CLASSES 0
+#endif
 #ifndef RTC_CHAIN_WGS_HIT
 #define RTC_CHAIN_WGS_HIT 4 /* whole frames of scenes whose bounce-hit share (bounce_hit_share) exceeds RTC_WGS_HIT_SHARE */
 #endif
@@ -1300,8 +1315,8 @@ constexpr int kDiagSects = 24;
 __device__ unsigned long long g_rtc_sect[kDiagSects]; /* [8..12] window statistics (rtc_render_chain) */
 /* rtc_render_chain's waves: (start, end, items) by s_memrealtime (the 100 MHz constant clock, the same on every
  * CU), one record per wave of the last launches until the log is full (rtc_diag_wavelog) */
-constexpr int kWaveLog = 16384;
-__device__ unsigned long long g_rtc_wavelog[kWaveLog][3];
+constexpr int kWaveLog = 16384, kWaveLogCols = 8; /* start, end, items, the end of items 1..5 */
+__device__ unsigned long long g_rtc_wavelog[kWaveLog][kWaveLogCols];
 __device__ unsigned g_rtc_wavecount;
 extern "C" int rtc_diag_wavelog(unsigned long long *out, int maxWaves, int reset)
 {
@@ -1310,7 +1325,7 @@ extern "C" int rtc_diag_wavelog(unsigned long long *out, int maxWaves, int reset
     n = std::min<unsigned>(n, (unsigned)kWaveLog);
     if (out && maxWaves > 0)
         HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_wavelog),
-                                    std::min<unsigned>(n, (unsigned)maxWaves) * 3 * sizeof(unsigned long long)));
+                                    std::min<unsigned>(n, (unsigned)maxWaves) * kWaveLogCols * sizeof(unsigned long long)));
     if (reset) {
         const unsigned z = 0;
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_wavecount), &z, sizeof z));
@@ -1527,6 +1542,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
                                                        unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
                                                        unsigned long long *__restrict__ pixMask)
 {
+#if RTC_CULL_PRIO > 0
+    __builtin_amdgcn_s_setprio(RTC_CULL_PRIO);
+#endif
     __shared__ unsigned wgWeight, wgAny;
     extern __shared__ unsigned long long sBlockCand[]; /* maskWords: the block's 16x16 prefilter survivors */
     CSTAMP(c0);
@@ -1587,6 +1605,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 #endif
     const PixelRay px = pixel_ray(P, bx, by);
     bool anyCand = false;
+    int nCand = 0; /* the tile's candidates (RTC_GEO_CLASSES) */
     /* level 2: the tile's own prefilter on the block's survivors, then the per-pixel filter */
     const TileCone K = tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2));
     for (int w = 0; w < P.maskWords; ++w) {
@@ -1617,6 +1636,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 #endif
         if (lane == 0)
             out[w] = bits;
+        nCand += __popcll(bits);
     }
     /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
      * non-empty candidate list exactly when its weight is > 0 */
@@ -1626,8 +1646,15 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         pixMask[tile] = b;
     }
     if (P.geoList && b) {
-        /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work) */
+        /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work); RTC_GEO_CLASSES:
+         * sub-list 4 c + tile % 4 for the class c of the tile's candidate count, the tiles with the longest lists (the
+         * dearest pixels: every sample tests them) first in the concatenated item order */
+#if RTC_GEO_CLASSES
+        const int cls = nCand >= 32 ? 0 : nCand >= 16 ? 1 : nCand >= 8 ? 2 : 3;
+        const int l = cls * 4 + (tile & 3);
+#else
         const int l = tile % kGeoLists;
+#endif
         int base = 0;
         if (lane == 0)
             base = atomicAdd(&P.geoCount[l * kGeoCountStride], __popcll(b));
@@ -2674,11 +2701,15 @@ template <bool MULTI, bool COUNT> /* MULTI: more than one chunk of clusters (chu
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
+#if RTC_CHAIN_PRIO > 0
+    __builtin_amdgcn_s_setprio(RTC_CHAIN_PRIO);
+#endif
     DSECT_BEGIN(dtot);
     DMARK_INIT(dcur);
 #ifdef RTC_DIAG
     const unsigned long long dWaveT0 = __builtin_amdgcn_s_memrealtime();
     unsigned dWaveItems = 0;
+    unsigned long long dItemEnd[5] = {0, 0, 0, 0, 0};
 #endif
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
@@ -3063,6 +3094,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
         it = itNext;
 #ifdef RTC_DIAG
+        if (dWaveItems < 5)
+            dItemEnd[dWaveItems] = __builtin_amdgcn_s_memrealtime();
         dWaveItems++;
 #endif
         DMARK(dcur, 18); /* item tail: the pixel's colour */
@@ -3093,6 +3126,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             g_rtc_wavelog[w][0] = dWaveT0;
             g_rtc_wavelog[w][1] = __builtin_amdgcn_s_memrealtime();
             g_rtc_wavelog[w][2] = dWaveItems;
+            for (int q = 0; q < 5; ++q)
+                g_rtc_wavelog[w][3 + q] = dItemEnd[q];
         }
     }
 #endif
@@ -3253,7 +3288,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     const dim3 superGrid((grid.x + kSuperBlocks - 1) / kSuperBlocks, (grid.y + kSuperBlocks - 1) / kSuperBlocks);
     const size_t superBytes = RTC_CULL_SUPER ? (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long) : 0;
-    const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64);
+    /* (RTC_GEO_CLASSES: a sub-list may receive every tile of a quarter -- all of one class) */
+    const int geoCap = (int)((tiles + (RTC_GEO_CLASSES ? 4 : kGeoLists) - 1) / (RTC_GEO_CLASSES ? 4 : kGeoLists) * 64);
     /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
      * that counts segments joins, the reduction reads the sky kernel's counters) */
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;

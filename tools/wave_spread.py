@@ -34,7 +34,7 @@ st = torch.cuda.Stream()
 for _ in range(5):
     ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, buf.data_ptr(), stream=st.cuda_stream)
 torch.cuda.synchronize()
-out = np.zeros((16384, 3), np.uint64)
+out = np.zeros((16384, 8), np.uint64)
 for rep in range(3):
     L.rtc_diag_wavelog(None, 0, 1)
     ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, buf.data_ptr(), stream=st.cuda_stream)
@@ -44,10 +44,18 @@ for rep in range(3):
     t0 = a[:, 0].min()
     start, end, items = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0, a[:, 2]  # 100 MHz ticks -> us
     q = lambda v, p: round(float(np.percentile(v, p)), 2)  # noqa: E731
+    ends = a[:, 3:8]  # the end of items 1..5 (0: not reached)
+    prev = a[:, 0].copy()
+    item_us = []
+    for k in range(5):
+        ok = ends[:, k] > 0
+        item_us.append(round(float(((ends[ok, k] - prev[ok]) / 100.0).mean()), 2) if ok.any() else None)
+        prev = np.where(ok, ends[:, k], prev)
     print(json.dumps({"scene": scene_name, "W": W, "H": H, "spp": SPP, "G": G, "waves": int(n), "items": int(items.sum()),
                       "span_us": round(float(end.max()), 2), "start_p50_us": q(start, 50), "start_max_us": q(start, 100),
                       "end_p10_us": q(end, 10), "end_p50_us": q(end, 50), "end_p90_us": q(end, 90),
                       "end_p99_us": q(end, 99), "items_p50": q(items, 50), "items_max": int(items.max()),
                       "busy_mean_us": round(float((end - start).mean()), 2),
-                      "busy_frac_of_span": round(float((end - start).sum() / (n * end.max())), 3)}), flush=True)
+                      "busy_frac_of_span": round(float((end - start).sum() / (n * end.max())), 3),
+                      "item_us_1_to_5": item_us}), flush=True)
 ds.close()
