@@ -267,8 +267,9 @@ def main():
     ap.add_argument("--band", default="auto",
                     help="N > 1 partition: rows per interleaved band (1: rows y = r + kN as main.c:84; 8: north_star's "
                          "row-tile split, bands of 8 rows).  auto: the faster one per frame size as measured on MI355X "
-                         "(profiles/r05_*_scale*: 1080p rows (the 8-row bands' 1/8 shares are less balanced: 4.46x vs "
-                         "4.50x), 4K bands of 8 (6.69x vs 6.48x))")
+                         "(profiles/r05_*_rank_share_overlap.log, r05_f_scale*: 1080p rows (the 8-row bands' 1/8 shares "
+                         "are less balanced: final tree 5.03x vs 4.47x), 4K bands of 8 (6.71x vs 6.68x, the mean of five "
+                         "runs))")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: process group backend.  nccl (= RCCL, the default) needs a GPU per rank; gloo is an "
                          "explicit rehearsal mode in which ranks may share GPUs (no RCCL leg; the line then reports "
