@@ -161,6 +161,12 @@ constexpr int kSkySlots = 8;
 #ifndef RTC_CULL_PRIO
 #define RTC_CULL_PRIO 0
 #endif
+/* Small shares of more pixels (the 1080p 1/4 share, 518 k px) run the tile cull at issue priority 3 as well: the next
+ * share's cull then competes on equal terms with this share's geometry kernel (1/4 share 0.1205 -> 0.1170 ms; the 1/8
+ * share measured no better that way, profiles/r05_cpq_ab_cull_priority.log) */
+#ifndef RTC_CULL_PRIO_MIN_PIXELS
+#define RTC_CULL_PRIO_MIN_PIXELS 400000
+#endif
 /* Wave priority of the geometry kernel (s_setprio): its waves are issued before the sky pass's on a shared SIMD.  A row
  * share's chain kernel runs ~3 pixels per wave; as its waves retire, sky waves fill their slots and the remaining chain
  * waves -- the share's critical path -- got a sixth of the issue: a wave's third and fourth pixels took 2-7x its first
@@ -789,6 +795,7 @@ struct RenderParams {
     int *__restrict__ geoCountNext; /* the next split launch's counters, zeroed by this launch's rtc_tile_cull */
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
+    int cullPrio; /* rtc_tile_cull's waves at issue priority 3 (RTC_CULL_PRIO_MIN_PIXELS) */
     int blocksX; /* 16x16 blocks per row of the launch */
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
@@ -1544,6 +1551,9 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 {
 #if RTC_CULL_PRIO > 0
     __builtin_amdgcn_s_setprio(RTC_CULL_PRIO);
+#else
+    if (KARG(cullPrio)) /* (RenderParams::cullPrio) */
+        __builtin_amdgcn_s_setprio(3);
 #endif
     __shared__ unsigned wgWeight, wgAny;
     extern __shared__ unsigned long long sBlockCand[]; /* maskWords: the block's 16x16 prefilter survivors */
@@ -3399,6 +3409,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
         P.geoList = order + blocks + 4 + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
+        P.cullPrio = smallShare && (size_t)d->width * (size_t)rows > (size_t)RTC_CULL_PRIO_MIN_PIXELS;
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
          * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
