@@ -228,6 +228,9 @@ __device__ __forceinline__ V3 random_direction(unsigned &s, const rtcmath::BmLog
     }
 #ifndef RTC_AB_NO_BM_FALLBACK /* timing experiment only (the exact fallback's register cost): not the reference */
     if (__builtin_expect(!ok, 0)) {
+#ifdef RTC_DIAG_BMFALL /* diagnostic builds: the lanes that take the fallback, per wave slot (rtc_diag_itemlog) */
+        atomicAdd(&g_rtc_bmfall[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 65535u], 1u);
+#endif
         s = s0;
         random_normals_exact(s, v);
     }
@@ -290,6 +293,23 @@ struct PowTablesLds {
     {
         e.log2tab = log2tab;
         e.exp2tab = exp2tab;
+    }
+};
+
+/* The certified Box-Muller tables (rtc_bm_tables.h) staged in LDS by a workgroup (call before its first __syncthreads;
+ * 192 threads fill them): random_direction's six lookups per draw are then LDS reads instead of global loads, which a
+ * hit's shading waited for on vmcnt behind the wave's older loads */
+struct BmTablesLds {
+    rtcmath::BmLogEntry log[128];
+    double cos[64][2];
+    __device__ __forceinline__ void fill(int tid)
+    {
+        if (tid < 128)
+            log[tid] = rtcmath::kBmLogTab[tid];
+        else if (tid < 192) {
+            cos[tid - 128][0] = rtcmath::kBmCosTab[tid - 128][0];
+            cos[tid - 128][1] = rtcmath::kBmCosTab[tid - 128][1];
+        }
     }
 };
 

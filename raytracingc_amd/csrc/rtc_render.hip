@@ -26,6 +26,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#ifdef RTC_DIAG
+#define RTC_DIAG_BMFALL 1
+__device__ unsigned g_rtc_bmfall[65536]; /* Box-Muller exact fallbacks per wave slot (diagnostic builds) */
+#endif
 
 #include "../../include/rtc.h"
 #include "rtc_device.h"
@@ -189,6 +193,13 @@ constexpr int kSkySlots = 8;
 /* rtc_render_chain's geometry-pixel sub-lists: kGeoLists counters, kGeoCountStride ints (one 128-B line) apart; a ring
  * of kGeoRing counter sets of kGeoSetInts ints (see RtcDeviceScene::geoCounts) */
 constexpr int kGeoLists = 16, kGeoCountStride = 32;
+/* rtc_render_chain's item counters (RTC_ITEM_COUNTERS > 0): counter x at geoCount[x * kGeoCountStride +
+ * kItemCounterOffset] (the line of sub-list x's count, which only rtc_tile_cull updates), zeroed with the counts */
+#ifndef RTC_ITEM_COUNTERS
+#define RTC_ITEM_COUNTERS 0 /* 0: the workgroup's LDS counter (see rtc_render_chain) */
+#endif
+constexpr int kItemCounters = RTC_ITEM_COUNTERS, kItemCounterOffset = 16;
+static_assert(kItemCounters <= kGeoLists, "one item counter per sub-list line at most");
 constexpr int kGeoRing = 16, kGeoSetInts = kGeoLists * kGeoCountStride;
 static_assert(kGeoSetInts >= kGeoLists * kGeoCountStride, "a counter set holds every sub-list counter");
 struct SkyKey {
@@ -966,8 +977,11 @@ __global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict_
                                                         int *__restrict__ geoCount)
 {
     const int t = blockIdx.x * 64 + threadIdx.x;
-    if (geoCount && blockIdx.x == 0 && threadIdx.x < kGeoLists) /* the launch's geometry sub-lists start empty */
+    if (geoCount && blockIdx.x == 0 && threadIdx.x < kGeoLists) { /* the launch's geometry sub-lists start empty */
         geoCount[threadIdx.x * kGeoCountStride] = 0;
+        if (threadIdx.x < kItemCounters)
+            geoCount[threadIdx.x * kGeoCountStride + kItemCounterOffset] = 0;
+    }
     if (t >= triCount)
         return;
     const DevTri T = tris[t];
@@ -1320,24 +1334,54 @@ extern "C" int rtc_diag_set_buffer(void *dptr)
  * 2 general filter loop, 3 general exact loop, 4 lane reduction, 5 hit shading, 6 sky (miss), 7 loop total */
 constexpr int kDiagSects = 24;
 __device__ unsigned long long g_rtc_sect[kDiagSects]; /* [8..12] window statistics (rtc_render_chain) */
-/* rtc_render_chain's waves: (start, end, items) by s_memrealtime (the 100 MHz constant clock, the same on every
- * CU), one record per wave of the last launches until the log is full (rtc_diag_wavelog) */
-constexpr int kWaveLog = 16384, kWaveLogCols = 8; /* start, end, items, the end of items 1..5 */
+/* rtc_render_chain's diagnostics, written with plain stores to per-wave-slot / per-item addresses (no same-address global
+ * atomics: thousands of them queued at a kernel's end held up other waves' memory operations behind them in the L2
+ * channels and made the tail look slow):
+ *   g_rtc_wavelog[slot]: start, end, items, the end of items 1..5 (s_memrealtime, the 100 MHz constant clock);
+ *   g_rtc_sectw[slot]: the wave's section cycles (s_rtc_sect) and window statistics, summed by rtc_diag_sections;
+ *   g_rtc_itemlog[item]: (start, end), (windows | tile candidates << 16 | wave slot << 32), (bounce iterations |
+ *     Box-Muller fallback lanes << 16 | triangle tests of the window lanes << 32, RTC_DIAG_COUNT builds only);
+ *   g_rtc_itemsect[item]: the item's cycles in sections kItemSectIds (s_memtime deltas). */
+constexpr int kWaveLog = 16384, kWaveLogCols = 8;
 __device__ unsigned long long g_rtc_wavelog[kWaveLog][kWaveLogCols];
-__device__ unsigned g_rtc_wavecount;
+__device__ unsigned long long g_rtc_sectw[kWaveLog][kDiagSects];
+constexpr int kItemLog = 1 << 18, kItemSectLog = 1 << 17, kItemSects = 16;
+__device__ unsigned long long g_rtc_itemlog[kItemLog][4];
+__device__ unsigned g_rtc_itemsect[kItemSectLog][kItemSects];
+__device__ __forceinline__ int item_sect_id(int k) /* the sections of g_rtc_itemsect's columns */
+{
+    return k < 10 ? k : (k == 10 ? 14 : k + 4); /* columns 0..9: sections 0..9; 10: 14; 11..15: 15..19 */
+}
+template <typename T> static int diag_zero(const T &sym)
+{
+    void *p = nullptr;
+    HIP_TRY(hipGetSymbolAddress(&p, HIP_SYMBOL(sym)));
+    HIP_TRY(hipMemset(p, 0, sizeof(T)));
+    return 0;
+}
+extern "C" int rtc_diag_itemlog(unsigned long long *out, int maxItems)
+{
+    const int n = std::min(maxItems, kItemLog);
+    if (out && n > 0)
+        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_itemlog), (size_t)n * 4 * sizeof(unsigned long long)));
+    return n;
+}
+extern "C" int rtc_diag_itemsect(unsigned *out, int maxItems)
+{
+    const int n = std::min(maxItems, kItemSectLog);
+    if (out && n > 0)
+        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_itemsect), (size_t)n * kItemSects * sizeof(unsigned)));
+    return n;
+}
+/* the wave records of the last launches (rows with a zero start: no wave); returns the slots copied */
 extern "C" int rtc_diag_wavelog(unsigned long long *out, int maxWaves, int reset)
 {
-    unsigned n = 0;
-    HIP_TRY(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rtc_wavecount), sizeof n));
-    n = std::min<unsigned>(n, (unsigned)kWaveLog);
-    if (out && maxWaves > 0)
-        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_wavelog),
-                                    std::min<unsigned>(n, (unsigned)maxWaves) * kWaveLogCols * sizeof(unsigned long long)));
-    if (reset) {
-        const unsigned z = 0;
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_wavecount), &z, sizeof z));
-    }
-    return (int)n;
+    const int n = std::min(maxWaves, kWaveLog);
+    if (out && n > 0)
+        HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_wavelog), (size_t)n * kWaveLogCols * sizeof(unsigned long long)));
+    if (reset && diag_zero(g_rtc_wavelog))
+        return -1;
+    return n;
 }
 #define CSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 /* per-block records of rtc_tile_cull (wave 0): {start, level 1 done, end, geometry, level-2 prefilter cycles, candidate
@@ -1377,11 +1421,18 @@ __shared__ unsigned long long s_rtc_sect[4][kDiagSects]; /* [wave][section]: 0..
 extern "C" int rtc_diag_sections(unsigned long long *out, int reset)
 {
     /* out: kDiagSects (24) counters */
-    if (out)
+    if (out) {
         HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtc_sect), kDiagSects * sizeof(unsigned long long)));
+        std::vector<unsigned long long> w((size_t)kWaveLog * kDiagSects);
+        HIP_TRY(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_rtc_sectw), w.size() * sizeof(unsigned long long)));
+        for (size_t i = 0; i < w.size(); ++i)
+            out[i % kDiagSects] += w[i];
+    }
     if (reset) {
         unsigned long long z[kDiagSects] = {0};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rtc_sect), z, sizeof z));
+        if (diag_zero(g_rtc_sectw))
+            return -1;
     }
     return 0;
 }
@@ -1564,8 +1615,11 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     }
     const int bx = blockIdx.x, by = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (P.geoCountNext && bx == 0 && by == 0 && threadIdx.x < kGeoLists) /* the next split launch's sub-lists */
+    if (P.geoCountNext && bx == 0 && by == 0 && threadIdx.x < kGeoLists) { /* the next split launch's sub-lists */
         P.geoCountNext[threadIdx.x * kGeoCountStride] = 0;
+        if (threadIdx.x < kItemCounters) /* and its geometry kernel's item counters */
+            P.geoCountNext[threadIdx.x * kGeoCountStride + kItemCounterOffset] = 0;
+    }
 #ifndef RTC_TILE_PREFILTER
 #define RTC_TILE_PREFILTER 1
 #endif
@@ -2304,7 +2358,11 @@ static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a fu
 static_assert(RTC_CHAIN_PAIRS * sizeof(unsigned short) >= 3 * 64 * sizeof(float), "a window's staged samples fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
-constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
+#ifndef RTC_BM_LDS
+#define RTC_BM_LDS 0 /* 1: the Box-Muller tables in LDS (BmTablesLds; round 5: frame and shares unchanged, chain -1 %) */
+#endif
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (RTC_BM_LDS ? sizeof(BmTablesLds) : 0) +
+                                   (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
                                    kChunkClusters * sizeof(DevCluster) /* sCl (RTC_DENSE_CULL) */;
 constexpr size_t kCuLds = 160 * 1024; /* gfx950 LDS per CU */
 /* the block LDS that keeps the chain workgroups per CU at most n: above kCuLds / (n + 1) */
@@ -2723,6 +2781,14 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
+#if RTC_BM_LDS
+    __shared__ BmTablesLds sBm;
+    static_assert(kChainBlock >= 192, "BmTablesLds::fill takes 192 threads");
+    sBm.fill(threadIdx.x);
+#define RTC_CHAIN_BM_TABS , sBm.log, sBm.cos
+#else
+#define RTC_CHAIN_BM_TABS
+#endif
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
 #if RTC_DENSE_CULL
@@ -2757,12 +2823,27 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * shortened the kernel 4 % but made every workgroup retire at its end, so the sky pass no longer filled the
      * tail: frame 0.396 -> 0.42 ms). */
     int nextIt = 0;
+#if RTC_ITEM_COUNTERS > 0
+    /* Experiment (round 5, not kept): global counters.  With a fixed 1/grid of the items per workgroup the
+     * workgroups' totals differ (item costs vary ~5x): at 1080p the kernel's span is ~20 % past its waves' mean busy
+     * time (per-item timings, tools/item_spread.py).  Here workgroup b takes items c + k * kItemCounters, c = b %
+     * kItemCounters (XCD b % 8 with 8), k from counter c, one returning atomic per item issued one item ahead.  The
+     * kernel got 6 % shorter but the frame 3-4 % longer (the sky pass no longer fills its tail) and the small shares
+     * 17-28 % longer (the counters saturate: ~30 atomics per us on one address); profiles/r05_xc_ab_item_counters.log */
+    int *const itemCounter = P.geoCount + ((int)blockIdx.x % kItemCounters) * kGeoCountStride + kItemCounterOffset;
+#define RTC_NEXT_ITEM() ((int)blockIdx.x % kItemCounters + atomicAdd(itemCounter, 1) * kItemCounters)
+#else
 #define RTC_NEXT_ITEM() ((int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x)
+#endif
     if (lane == 0)
         nextIt = RTC_NEXT_ITEM();
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
      * segment where they are used: KARG) */
+#ifdef RTC_DIAG_COUNT /* diagnostic variant: the test counters on in every launch (rtc_diag_itemlog's tests) */
+    constexpr bool counting = true;
+#else
     constexpr bool counting = COUNT;
+#endif
     unsigned segCalls = 0, segTraced = 0, segClusters = 0;
     unsigned long long segTests = 0, segSpec = 0;
 #ifdef RTC_DIAG
@@ -2810,6 +2891,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     for (;;) {
         if (it >= nItems)
             break;
+#ifdef RTC_DIAG
+        const unsigned long long dItemT0 = __builtin_amdgcn_s_memrealtime();
+        unsigned dItemWindows = 0;
+        const unsigned long long dItemIters0 = dIters;
+        const unsigned dBm0 = __atomic_load_n(&g_rtc_bmfall[(blockIdx.x * (kChainBlock / 64) + (threadIdx.x >> 6)) & 65535u],
+                                              __ATOMIC_RELAXED);
+        const unsigned long long dSect = lane < kItemSects ? s_rtc_sect[threadIdx.x >> 6][item_sect_id(lane)] : 0ull;
+        unsigned long long dItemTests = 0;
+#endif
 #if RTC_ITEM_PREFETCH
         const int code = __builtin_amdgcn_readfirstlane((int)vc);
         const unsigned long long m0 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 0) |
@@ -2932,6 +3022,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
                         DevTri T;
                         DevMat M;
+                        DSECT_BEGIN(dh8);
                         if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
                             const int u = __builtin_amdgcn_readfirstlane(c.idx);
                             T = KLOAD(KARG(tris), u);
@@ -2940,6 +3031,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             T = P.tris[c.idx]; /* (kernel-argument pointers: global loads, not flat) */
                             M = P.mats[c.idx];
                         }
+#ifdef RTC_DIAG_HITSPLIT /* diagnostic: the hit's loads (and any older ones still in flight) apart from its draws */
+                        __builtin_amdgcn_s_waitcnt(0);
+                        DSECT_END(dh8, 8);
+#endif
+                        DSECT_BEGIN(dh9);
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
 #if RTC_DRAW_TABLE
                         /* the hit draws (see RTC_DRAW_TABLE): the primary hit computes the lane's own and enters
@@ -2948,16 +3044,19 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         float4 D;
                         if (first || lane + iter >= nAct) {
                             unsigned s = first ? rng : rng * J.a + J.c;
-                            const V3 rd = random_direction(s);
+                            const V3 rd = random_direction(s RTC_CHAIN_BM_TABS);
                             D = make_float4(rd.x, rd.y, rd.z, random_value(s));
                             if (first)
                                 W.draw[lane] = D; /* read in later iterations, after chain_trace_pairs' LDS syncs */
                         } else {
                             D = W.draw[lane + iter];
                         }
+#ifdef RTC_DIAG_HITSPLIT
+                        DSECT_END(dh9, 9);
+#endif
                         const V3 diffuseDir = normalized(add(normal, V3{D.x, D.y, D.z}));
 #else
-                        const V3 diffuseDir = normalized(add(normal, random_direction(rng)));
+                        const V3 diffuseDir = normalized(add(normal, random_direction(rng RTC_CHAIN_BM_TABS)));
 #endif
                         const V3 specularDir = reflect(dir, normal);
                         dir = lerp(diffuseDir, specularDir, M.smoothness);
@@ -3076,6 +3175,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 flush();
             jn += (unsigned)p;
 #ifdef RTC_DIAG
+            {
+                unsigned long long tw = act ? tests : 0u;
+                for (int o = 32; o > 0; o >>= 1)
+                    tw += __shfl_xor(tw, o);
+                dItemTests += tw;
+            }
+            dItemWindows++;
             dWindows++;
             dAct += (unsigned)nAct;
             dUsed += (unsigned long long)__popcll(__ballot(mult > 0));
@@ -3102,6 +3208,20 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
         if (!maskNext) /* (an item without a bounce iteration) */
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+#ifdef RTC_DIAG
+        if (lane == 0 && it < kItemLog) {
+            g_rtc_itemlog[it][0] = dItemT0;
+            g_rtc_itemlog[it][1] = __builtin_amdgcn_s_memrealtime();
+            g_rtc_itemlog[it][2] = (unsigned long long)dItemWindows |
+                                   (unsigned long long)(__popcll(m0) + __popcll(m1)) << 16 |
+                                   (unsigned long long)(blockIdx.x * (kChainBlock / 64) + (threadIdx.x >> 6)) << 32;
+            const unsigned dBm1 = __atomic_load_n(
+                &g_rtc_bmfall[(blockIdx.x * (kChainBlock / 64) + (threadIdx.x >> 6)) & 65535u], __ATOMIC_RELAXED);
+            g_rtc_itemlog[it][3] = (dIters - dItemIters0) | (unsigned long long)(dBm1 - dBm0) << 16 | dItemTests << 32;
+        }
+        if (it < kItemSectLog && lane < kItemSects)
+            g_rtc_itemsect[it][lane] = (unsigned)(s_rtc_sect[threadIdx.x >> 6][item_sect_id(lane)] - dSect);
+#endif
         it = itNext;
 #ifdef RTC_DIAG
         if (dWaveItems < 5)
@@ -3113,32 +3233,26 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     DMARK(dcur, 15);
 #ifdef RTC_DIAG
     DSECT_END(dtot, 13);
-    if (lane < 8 || (lane >= 13 && lane < 22))
-        atomicAdd(&g_rtc_sect[lane], s_rtc_sect[threadIdx.x >> 6][lane]);
-    /* [8] bounce-loop iterations, [9] live lanes summed over them, [10] window lanes, [11] windows, [12] lanes
-     * whose sample was used */
-    if (lane == 0) {
-        atomicAdd(&g_rtc_sect[8], dIters);
-        atomicAdd(&g_rtc_sect[9], dAlive);
-        atomicAdd(&g_rtc_sect[10], dAct);
-        atomicAdd(&g_rtc_sect[11], dWindows);
-        atomicAdd(&g_rtc_sect[12], dUsed);
-        atomicAdd(&g_rtc_sect[22], dIters2); /* [22] iterations of later bounces, [23] their live lanes */
-        atomicAdd(&g_rtc_sect[23], dAlive2);
+    {
+        /* per-slot plain stores (see g_rtc_sectw): lanes 0..7, 13..21 the sections, 8..12 and 22, 23 the window statistics */
+        const unsigned slotW = (blockIdx.x * (kChainBlock / 64) + (threadIdx.x >> 6)) % (unsigned)kWaveLog;
+        unsigned long long v = lane < kDiagSects ? s_rtc_sect[threadIdx.x >> 6][lane] : 0ull;
+        v = lane == 8 ? dIters : lane == 9 ? dAlive : lane == 10 ? dAct : lane == 11 ? dWindows : lane == 12 ? dUsed : v;
+        v = lane == 22 ? dIters2 : lane == 23 ? dAlive2 : v;
+        if (lane < kDiagSects)
+            g_rtc_sectw[slotW][lane] = v;
     }
 #endif
     if (counting)
         flush_counters(P, segCalls, segTraced, segTests, lane, segClusters, segSpec);
 #ifdef RTC_DIAG
     if (lane == 0) {
-        const unsigned w = atomicAdd(&g_rtc_wavecount, 1u);
-        if (w < (unsigned)kWaveLog) {
-            g_rtc_wavelog[w][0] = dWaveT0;
-            g_rtc_wavelog[w][1] = __builtin_amdgcn_s_memrealtime();
-            g_rtc_wavelog[w][2] = dWaveItems;
-            for (int q = 0; q < 5; ++q)
-                g_rtc_wavelog[w][3 + q] = dItemEnd[q];
-        }
+        const unsigned w = (blockIdx.x * (kChainBlock / 64) + (threadIdx.x >> 6)) % (unsigned)kWaveLog;
+        g_rtc_wavelog[w][0] = dWaveT0;
+        g_rtc_wavelog[w][1] = __builtin_amdgcn_s_memrealtime();
+        g_rtc_wavelog[w][2] = dWaveItems;
+        for (int q = 0; q < 5; ++q)
+            g_rtc_wavelog[w][3 + q] = dItemEnd[q];
     }
 #endif
 }

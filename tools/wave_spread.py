@@ -40,7 +40,8 @@ for rep in range(3):
     ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, buf.data_ptr(), stream=st.cuda_stream)
     torch.cuda.synchronize()
     n = L.rtc_diag_wavelog(out.ctypes.data, 16384, 1)
-    a = out[:n].astype(np.int64)
+    a = out[:n][out[:n, 0] != 0].astype(np.int64)  # slots with a wave
+    n = len(a)
     t0 = a[:, 0].min()
     start, end, items = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0, a[:, 2]  # 100 MHz ticks -> us
     q = lambda v, p: round(float(np.percentile(v, p)), 2)  # noqa: E731
