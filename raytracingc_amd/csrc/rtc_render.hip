@@ -180,6 +180,14 @@ constexpr int kSkySlots = 8;
 #ifndef RTC_CHAIN_PRIO
 #define RTC_CHAIN_PRIO 3
 #endif
+/* RTC_GEO_HINT (experiment, round 5, not kept): the tile cull puts the pixels that took more than one window in the
+ * previous launch's geometry kernel (a per-pixel byte the kernel sets) first in the item order -- the longest items
+ * first.  A scheduling hint: any hint contents give the same frame.  Measured (profiles/r05_gh_ab_geo_hint.log): the
+ * 1080p shares unchanged (consecutive pipelined shares already fill each other's tails), the whole frame's geometry
+ * kernel -3 % at the same frame time, fsuzane +4 % */
+#ifndef RTC_GEO_HINT
+#define RTC_GEO_HINT 0
+#endif
 #ifndef RTC_GEO_CLASSES
 #define RTC_GEO_CLASSES 0
 #endif
@@ -237,6 +245,8 @@ struct RtcDeviceScene {
      * each launch's tile cull zeroes the next launch's set, so a launch on the same stream as the previous one
      * needs no rtc_prep_primary to clear its counters (cullStream: that stream) */
     int *geoCounts;
+    unsigned char *tileHint; /* RTC_GEO_HINT: per pixel (tile * 64 + bit) of the last launches, 1 = several windows */
+    size_t tileHintCap;
     unsigned long long geoSeq;
     hipStream_t cullStream;
     bool cullValid;
@@ -738,6 +748,8 @@ extern "C" int rtc_scene_release(RtcDeviceScene *s)
         (void)hipFree(s->segSlots);
     if (s->geoCounts)
         (void)hipFree(s->geoCounts);
+    if (s->tileHint)
+        (void)hipFree(s->tileHint);
     if (s->evFork)
         (void)hipEventDestroy(s->evFork);
     if (s->evJoin)
@@ -807,6 +819,8 @@ struct RenderParams {
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
     int cullPrio; /* rtc_tile_cull's waves at issue priority 3 (RTC_CULL_PRIO_MIN_PIXELS) */
+    unsigned char *tileHint; /* RTC_GEO_HINT (null: none), per pixel tile * 64 + bit: read and cleared by rtc_tile_cull,
+                              * set by rtc_render_chain for pixels of more than one window */
     int blocksX; /* 16x16 blocks per row of the launch */
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
@@ -1710,23 +1724,37 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         pixMask[tile] = b;
     }
     if (P.geoList && b) {
-        /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work); RTC_GEO_CLASSES:
-         * sub-list 4 c + tile % 4 for the class c of the tile's candidate count, the tiles with the longest lists (the
-         * dearest pixels: every sample tests them) first in the concatenated item order */
+        /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work) */
+        const auto append = [&](unsigned long long gb, int l) {
+            int base = 0;
+            if (lane == 0)
+                base = atomicAdd(&P.geoCount[l * kGeoCountStride], __popcll(gb));
+            base = __builtin_amdgcn_readfirstlane(base);
+            /* a sub-list holds every geometry pixel of its tiles (geoCap = 64 x its tiles) when its counter started at
+             * 0; a stale counter must not write past it (the readers clamp the counts to geoCap too) */
+            if (((gb >> lane) & 1ull) && base + __popcll(gb) <= P.geoCap)
+                P.geoList[(size_t)l * P.geoCap + base + __popcll(gb & ((1ull << lane) - 1ull))] = tile * 64 + lane;
+        };
 #if RTC_GEO_CLASSES
+        /* sub-list 4 c + tile % 4 for the class c of the tile's candidate count, the tiles with the longest lists (the
+         * dearest pixels: every sample tests them) first in the concatenated item order */
         const int cls = nCand >= 32 ? 0 : nCand >= 16 ? 1 : nCand >= 8 ? 2 : 3;
-        const int l = cls * 4 + (tile & 3);
+        append(b, cls * 4 + (tile & 3));
+#elif RTC_GEO_HINT
+        /* the pixels the hint marks go to sub-lists 0-3 (the head of the item order), the tile's others to sub-lists 4-15
+         * spread by tile; sub-list l receives only pixels of tiles with tile % 4 == l % 4 (geoCap: a quarter of the
+         * tiles' pixels) */
+        const bool marked = P.tileHint && ((b >> lane) & 1ull) && P.tileHint[(size_t)tile * 64 + lane] != 0;
+        const unsigned long long hb = __ballot(marked);
+        if (marked)
+            P.tileHint[(size_t)tile * 64 + lane] = 0; /* this launch's geometry kernel marks it again */
+        if (hb)
+            append(hb, tile & 3);
+        if (b & ~hb)
+            append(b & ~hb, 4 * (1 + (tile >> 2) % 3) + (tile & 3));
 #else
-        const int l = tile % kGeoLists;
+        append(b, tile % kGeoLists);
 #endif
-        int base = 0;
-        if (lane == 0)
-            base = atomicAdd(&P.geoCount[l * kGeoCountStride], __popcll(b));
-        base = __builtin_amdgcn_readfirstlane(base);
-        /* a sub-list holds every geometry pixel of its tiles (geoCap = 64 x its tiles) when its counter started at 0;
-         * a stale counter must not write past it (the readers clamp the counts to geoCap too) */
-        if (((b >> lane) & 1ull) && base + __popcll(b) <= P.geoCap)
-            P.geoList[(size_t)l * P.geoCap + base + __popcll(b & ((1ull << lane) - 1ull))] = tile * 64 + lane;
     }
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
@@ -2952,7 +2980,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         float acc = 0.f;
         int k = 0;       /* samples accumulated */
         unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
+        int nWin = 0;    /* windows of this item (RTC_GEO_HINT) */
         while (k < P.spp && P.maxBounce > 0) {
+            ++nWin;
             /* window: the state indices the remaining samples likely span (the pixel's hits per sample so far, a
              * margin; the first window assumes one hit per sample) */
             const int need = P.spp - k;
@@ -3208,6 +3238,8 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
         if (!maskNext) /* (an item without a bounce iteration) */
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+        if (RTC_GEO_HINT && nWin > 1 && lane == 0 && KARG(tileHint)) /* the next launch's tile cull orders it first */
+            KARG(tileHint)[code] = 1;
 #ifdef RTC_DIAG
         if (lane == 0 && it < kItemLog) {
             g_rtc_itemlog[it][0] = dItemT0;
@@ -3413,7 +3445,8 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     const dim3 superGrid((grid.x + kSuperBlocks - 1) / kSuperBlocks, (grid.y + kSuperBlocks - 1) / kSuperBlocks);
     const size_t superBytes = RTC_CULL_SUPER ? (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long) : 0;
     /* (RTC_GEO_CLASSES: a sub-list may receive every tile of a quarter -- all of one class) */
-    const int geoCap = (int)((tiles + (RTC_GEO_CLASSES ? 4 : kGeoLists) - 1) / (RTC_GEO_CLASSES ? 4 : kGeoLists) * 64);
+    const int geoLanes = RTC_GEO_CLASSES || RTC_GEO_HINT ? 4 : kGeoLists; /* (RTC_GEO_HINT: likewise) */
+    const int geoCap = (int)((tiles + geoLanes - 1) / geoLanes * 64);
     /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
      * that counts segments joins, the reduction reads the sky kernel's counters) */
     const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
@@ -3524,6 +3557,18 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.geoList = order + blocks + 4 + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
         P.cullPrio = smallShare && (size_t)d->width * (size_t)rows > (size_t)RTC_CULL_PRIO_MIN_PIXELS;
+        if (RTC_GEO_HINT) { /* grown on demand (hipFree synchronises: no launch still uses the old one) */
+            if (tiles * 64 > s->tileHintCap) {
+                if (ms->tileHint)
+                    HIP_TRY(hipFree(ms->tileHint));
+                ms->tileHint = nullptr;
+                ms->tileHintCap = 0;
+                HIP_TRY(hipMalloc((void **)&ms->tileHint, tiles * 64));
+                HIP_TRY(hipMemset(ms->tileHint, 0, tiles * 64));
+                ms->tileHintCap = tiles * 64;
+            }
+            P.tileHint = s->tileHint;
+        }
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
          * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64

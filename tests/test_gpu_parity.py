@@ -210,6 +210,49 @@ def test_chain_occupancy_hint(gpu_available):
         ds.close()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+def test_tile_hint_order_same_frame(overlap, gpu_available):
+    """Repeated launches of one DeviceScene interleaved with launches of another camera and another row share all
+    equal the oracle bit for bit: nothing a launch leaves in the scene's buffers (counter sets, scratch slots, and in
+    builds with RTC_GEO_HINT the per-pixel order hint the geometry kernel sets for the next tile cull) changes a
+    later frame."""
+    import torch
+
+    from raytracingc_amd.distributed import rank_config
+
+    tris, tonly = load_tris("fsuzane")
+    scene = rt.default_scene()
+    cam = rt.camera_basis()
+    cam2 = rt.camera_basis((1.5, 1.0, -6.0), (0.0, 1.0, 0.0), 1.2)
+    w, h, spp = 96, 64, 8
+    d = RtcRenderDesc(w, h, spp, 10, tonly, 0, 1, 0, 0)
+    ocol, oacc, _ = orc.render(tris, None, scene, cam, d, threads=8)
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    cfg = rt.RenderConfig(w, h, spp, 10, bool(tonly), overlap=overlap)
+    other = [(cam2, cfg), (cam, rank_config(cfg, 1, 2, band=8))]
+    got = []
+    for rep in range(4):
+        buf = torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda")
+        acc = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        ds.render_rows_async(scene, cam, cfg, buf.data_ptr(), accum_ptr=acc.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        got.append((buf.cpu().numpy(), acc.cpu().numpy()))
+        if rep >= 2:  # scramble the hint with other launches of the scene
+            for c, f in other:
+                junk = torch.zeros((max(f.rows(), 1), w, 3), dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                ds.render_rows_async(scene, c, f, junk.data_ptr(), stream=st.cuda_stream)
+                torch.cuda.synchronize()
+    ds.close()
+    nan = np.isnan(oacc)
+    for gcol, gacc in got:
+        assert np.array_equal(gcol, ocol)
+        assert np.array_equal(np.isnan(gacc), nan)
+        assert np.array_equal(_bits(gacc[~nan]), _bits(oacc[~nan]))
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_random_configurations_match_oracle(seed, gpu_available):
     """Randomised end-to-end parity against the CPU restatement (the oracle pinned to the reference's fixtures):
