@@ -2260,7 +2260,12 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
 #if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the environment's cost) */
                 const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y + (float)s * 1e-9f, 0.f));
 #else
-                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f})); /* raytracing.c:291 */
+                /* raytracing.c:291 with rayColor (1, 1, 1): 0 + environment (environment_miss_term: acc starts at +0) */
+#ifndef RTC_SKY_MISS_FULL
+                const V3 l = environment_miss_term(dir, P.env);
+#else /* the reference's adds as written (same values; round 5 A/B) */
+                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f}));
+#endif
 #endif
                 acc = add(acc, mul(l, P.invSpp)); /* main.c:99 */
             }
