@@ -3545,7 +3545,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         return 0;
     };
     const bool chain = fused;
-    unsigned long long *mask = cull ? (unsigned long long *)(s->scratch + (size_t)half * halfBytes) : nullptr;
+    /* slot `half` starts at half x (the allocation's slot size), not half x this launch's size: consecutive launches of
+     * different sizes (the last, shorter row share of a band partition, a whole frame after a share) are in flight
+     * together on the alternating streams, and with per-launch offsets a smaller launch's slot 1 overlapped the
+     * previous launch's slot 0 -- its tile cull overwrote the geometry list that launch's geometry kernel was reading
+     * (geometry pixels left unrendered; found by test_small_shares_sum_in_kernel[True-8-8], round 5) */
+    const size_t slotBytes = s->scratchCap / kSkySlots;
+    unsigned long long *mask = cull ? (unsigned long long *)(s->scratch + (size_t)half * slotBytes) : nullptr;
     unsigned long long *pixMask = cull ? mask + tiles * (size_t)s->maskWords : nullptr;
     unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
     unsigned *tileW = cull ? weight + blocks : nullptr;

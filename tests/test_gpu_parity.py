@@ -433,10 +433,53 @@ def test_small_shares_sum_in_kernel(overlap, G, band, gpu_available):
     ds.close()
     o, a = out.cpu().numpy(), acc.cpu().numpy()
     for r in range(G):
-        ys = band_rows(H, r, G, band)
+        ys = np.asarray(band_rows(H, r, G, band))
         n = len(ys)
-        assert np.array_equal(o[r, :n], ref[ys]), f"rank {r} bytes"
+        bad = np.nonzero(np.any(o[r, :n] != ref[ys], axis=2))
+        detail = ""
+        if len(bad[0]):
+            rr, xx = bad
+            detail = (f": {len(rr)} pixels, rows {sorted(set(int(ys[v]) for v in rr))[:12]}, x {int(xx.min())}..{int(xx.max())}, "
+                      f"first {[(int(ys[rr[k]]), int(xx[k]), o[r, rr[k], xx[k]].tolist(), ref[ys[rr[k]], xx[k]].tolist(), a[r, rr[k], xx[k]].tolist(), racc[ys[rr[k]], xx[k]].tolist()) for k in range(min(3, len(rr)))]}")
+        assert np.array_equal(o[r, :n], ref[ys]), f"rank {r} bytes{detail}"
         assert np.array_equal(_bits(a[r, :n]), _bits(racc[ys])), f"rank {r} floats"
+
+
+def test_mixed_size_overlapped_launches(gpu_available):
+    """Pipelined launches of different sizes in flight together on one scene: the 1080p band partition's rank 6 (17
+    bands, 128 spp: a long geometry kernel) and then rank 7 (16 bands, 1 spp), whose tile cull runs on the other cull
+    stream while rank 6's geometry kernel still reads its lists; then a whole small frame.  Each launch's scratch slot
+    must not overlap the slot of the launch running beside it (round 5: slot offsets were per-launch sizes, and rank 7's
+    tile cull overwrote rank 6's geometry list -- geometry pixels left unrendered)."""
+    import torch
+
+    from raytracingc_amd.distributed import band_rows, rank_config, rows_per_rank
+
+    tris, _ = load_tris("ultracomplex")
+    scene, cam, _ = setup_from_flags({})
+    W, H, G, band = 1920, 1080, 8, 8
+    plan = [(6, 128), (7, 1), (6, 128), (7, 1)]
+    refs = {spp: rt.render(tris, None, scene, cam, rt.RenderConfig(W, H, spp, 10, True))[0] for spp in (128, 1)}
+    sref, _, _ = rt.render(tris, None, scene, cam, rt.RenderConfig(200, 120, 16, 10, True))
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.current_stream().cuda_stream
+    rows = rows_per_rank(H, G, band)
+    out = torch.zeros((len(plan), rows, W, 3), dtype=torch.uint8, device="cuda")
+    sout = torch.zeros((120, 200, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    for i, (r, spp) in enumerate(plan):
+        cfg = rank_config(rt.RenderConfig(W, H, spp, 10, True, overlap=True), r, G, band)
+        ds.render_rows_async(scene, cam, cfg, out[i].data_ptr(), None, None, st)
+    ds.render_rows_async(scene, cam, rt.RenderConfig(200, 120, 16, 10, True, overlap=True), sout.data_ptr(), None, None,
+                         st)
+    torch.cuda.synchronize()
+    ds.close()
+    o = out.cpu().numpy()
+    for i, (r, spp) in enumerate(plan):
+        ys = np.asarray(band_rows(H, r, G, band))
+        bad = int(np.any(o[i, :len(ys)] != refs[spp][ys], axis=2).sum())
+        assert bad == 0, f"launch {i} (rank {r}, {spp} spp): {bad} pixels differ"
+    assert np.array_equal(sout.cpu().numpy(), sref)
 
 
 def test_device_scene_reuse_sizes_counters_timing(gpu_available):
