@@ -29,7 +29,7 @@ $(BUILD)/scene_build.o: $(CSRC)/scene_build.c $(CSRC)/rtc_internal.h include/rtc
 	$(CC) $(CFLAGS) -c $< -o $@
 
 # header dependencies: explicit below, and generated (-MMD) for anything the explicit lists miss
-HDRS     := $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_bm_tables.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h
+HDRS     := $(CSRC)/rtc_layout.h $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_bm_tables.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h
 -include $(wildcard $(BUILD)/*.d)
 
 $(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
@@ -38,7 +38,16 @@ $(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
 $(BUILD)/rtc_frame.o: $(CSRC)/rtc_frame.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
 
-$(LIB): $(BUILD)/rtc_render.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
+$(BUILD)/rtc_scene.o: $(CSRC)/rtc_scene.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+$(BUILD)/rtc_probe.o: $(CSRC)/rtc_probe.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+# the objects every library variant shares (the render kernels are rtc_render.o, or a variant of it)
+COMMON   := $(BUILD)/rtc_frame.o $(BUILD)/rtc_scene.o $(BUILD)/rtc_probe.o $(BUILD)/scene_build.o
+
+$(LIB): $(BUILD)/rtc_render.o $(COMMON)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl -L/opt/rocm/lib -lhsa-runtime64
 
 # diagnostic variant (per-wave cycle stamps); never the measured product
@@ -46,7 +55,7 @@ DIAGLIB  := $(LIBDIR)/librtc_diag.so
 $(BUILD)/rtc_render_diag.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DRTC_DIAG -MMD -MP -c $< -o $@
 
-$(DIAGLIB): $(BUILD)/rtc_render_diag.o $(BUILD)/rtc_frame.o $(BUILD)/scene_build.o
+$(DIAGLIB): $(BUILD)/rtc_render_diag.o $(COMMON)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -ldl -L/opt/rocm/lib -lhsa-runtime64
 
 diag: $(DIAGLIB)

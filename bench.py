@@ -281,7 +281,8 @@ def main():
     import torch.distributed as dist
 
     import raytracingc_amd as rt
-    from raytracingc_amd.distributed import SharedHostFrames, pin_rank_near_gpu, rank_config, rows_per_rank
+    from raytracingc_amd.distributed import (SharedHostFrames, pin_rank_near_gpu, rank_config, rank_report,
+                                             rows_per_rank)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -360,6 +361,8 @@ def main():
         return ds.frame_loop(scene, cams or cam, cfg, [t.data_ptr() for t in dev_rows], host_ptr, pitch, frames,
                              stream.cuda_stream)
 
+    local_s = [0.0]  # this rank's own time of the last timed region (rank_report)
+
     def timed(cfg, steps, warmup, cams=None):
         """warmup + steps pipelined frames (rtc_frame_loop: render with RTC_F_OVERLAP, each frame's rows copied into
         the host frame by the SDMA engines while the next frames render); the timed region spans the steps frames,
@@ -372,15 +375,19 @@ def main():
         st = loop(cfg, steps, cams)
         torch.cuda.synchronize(dev)
         barrier()
-        dt = allreduce_max(time.perf_counter() - t0)
+        local_s[0] = time.perf_counter() - t0
+        dt = allreduce_max(local_s[0])
         return dt, st
+
+    local_seg = [0] * rt.RTC_SEGMENT_COUNTERS  # this rank's own counters of the last counters() frame
 
     def counters(cfg):
         """the work counters of one more frame of the same configuration (untimed; every frame is identical)"""
         seg.zero_()
         ds.render_rows_async(scene, cam, cfg, dev_rows[0].data_ptr(), None, seg.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize(dev)
-        return allreduce_sum([int(v) for v in seg.tolist()])
+        local_seg[:] = [int(v) for v in seg.tolist()]
+        return allreduce_sum(list(local_seg))
 
     # untimed frames for ~0.3 s: the GPU clocks settle before the kernel timing and the timed region
     t_settle = time.perf_counter()
@@ -407,6 +414,9 @@ def main():
 
     t, lst = timed(cfg_r, args.steps, args.warmup)
     seg_calls, seg_traced, tri_tests, cluster_tests, discarded_tests = counters(cfg_r)
+    # N > 1: what the communicator reports (RCCL's rank count on the nccl backend) beside every rank's own ms and
+    # segment count
+    report = rank_report(local_s[0] / args.steps * 1e3, local_seg[0]) if multi else None
     samples = W * H * spp
     value = samples * args.steps / t / 1e6
     # the last frame of the timed run as it landed in host memory (every rank's rows)
@@ -555,6 +565,9 @@ def main():
             line["ranks"] = world
             line["ranks_per_gpu"] = round(world / n_phys, 3)
             line["rehearsal"] = backend == "gloo"
+            line["ranks_report"] = report
+            if backend == "nccl":
+                line["rccl_nranks"] = report["comm_world_size"]
         mcam = orbit[(args.steps - 1) % len(orbit)]
         refm, _, _ = rt.render(tris, None, scene, mcam, cfg_joined, device=gpu)
         moving["last_frame_equals_rtc_render"] = bool(np.array_equal(frame_mov, refm))

@@ -169,6 +169,11 @@ int rtc_render(const Triangle *tris, int triCount, const Sphere *spheres, int sp
 int rtc_render_multi(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount,
                      const Scene *scene, const RtcCamera *cam, const RtcRenderDesc *d, int numDevices,
                      Color *outImage, float *outAccum, RtcStats *stats);
+/* What the calling thread's last rtc_render_multi ran on: *path 0 (no call yet), 1 (RCCL gather) or 2 (RTC_F_HOST_ROWS,
+ * no communicator); *devices its numDevices; commRanks[g] (up to maxComms) the rank count communicator g reports itself
+ * (ncclCommCount; -1 if not reported).  Returns the number of communicators.  No reference counterpart: it shows that
+ * RCCL saw the whole clique (main.c:285-302's fan-out lifted to GPUs). */
+int rtc_last_multi_info(int *path, int *devices, int *commRanks, int maxComms);
 
 /* ---- render: device-resident (used by the multi-GPU host and bench) -------------------------------- */
 typedef struct RtcDeviceScene RtcDeviceScene;

@@ -211,6 +211,16 @@ def render_multi(tris, spheres, scene: Scene, cam: RtcCamera, cfg: RenderConfig,
     return colors, accum, _stats(st)
 
 
+def last_multi_info() -> dict:
+    """What this thread's last render_multi ran on (rtc_last_multi_info): path ("none" | "rccl" | "host_rows"), devices,
+    and per communicator the rank count RCCL itself reports (ncclCommCount)."""
+    path, devs = C.c_int(), C.c_int()
+    ranks = (C.c_int * 64)()
+    n = lib().rtc_last_multi_info(C.byref(path), C.byref(devs), ranks, 64)
+    return {"path": {0: "none", 1: "rccl", 2: "host_rows"}.get(path.value, str(path.value)), "devices": devs.value,
+            "comm_ranks": [int(ranks[i]) for i in range(min(n, 64))]}
+
+
 class DeviceScene:
     """A scene resident in HBM on one device (rtc_scene_upload).  render_rows_async takes raw device
     pointers and a hipStream_t (ints), e.g. from torch tensors / torch.cuda streams."""

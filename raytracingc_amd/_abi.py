@@ -134,7 +134,7 @@ EXPORTS = [
     "rtc_last_error", "rtc_version", "rtc_device_count",
     "rtc_load_obj", "rtc_parse_triangle_file", "rtc_free", "rtc_default_spheres", "rtc_default_scene",
     "rtc_scene_set_sun", "rtc_camera_basis", "rtc_write_bmp", "rtc_quantize",
-    "rtc_render", "rtc_render_multi",
+    "rtc_render", "rtc_render_multi", "rtc_last_multi_info",
     "rtc_scene_upload", "rtc_scene_release", "rtc_rows_selected", "rtc_render_rows_async", "rtc_scene_set_timing", "rtc_scene_kernel_times",
     "rtc_bounce_hit_share", "rtc_scene_chain_wgs",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
@@ -186,6 +186,7 @@ def lib() -> C.CDLL:
                              vp, vp, C.POINTER(RtcStats)]
     L.rtc_render_multi.argtypes = [vp, ip, vp, ip, C.POINTER(Scene), C.POINTER(RtcCamera),
                                    C.POINTER(RtcRenderDesc), ip, vp, vp, C.POINTER(RtcStats)]
+    L.rtc_last_multi_info.argtypes = [C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), ip]
     L.rtc_scene_upload.argtypes = [vp, ip, vp, ip, ip, C.POINTER(vp)]
     L.rtc_scene_release.argtypes = [vp]
     L.rtc_scene_kernel_times.argtypes = [vp, vp]

@@ -13,8 +13,7 @@
 
 /* Timing-experiment switches that change the frame (not the reference's arithmetic): a build defines one only together
  * with RTC_EXPERIMENT, which the Makefile's product targets never define. */
-#if (defined(RTC_AB_CHEAP_ENV_SKY) || defined(RTC_AB_CHEAP_ENV_CHAIN) || defined(RTC_AB_CHEAP_DIR) ||                 \
-     defined(RTC_AB_NO_BM_FALLBACK) || defined(RTC_AB_NO_SLOTS)) && !defined(RTC_EXPERIMENT)
+#if (defined(RTC_AB_CHEAP_ENV_SKY) || defined(RTC_AB_CHEAP_DIR) || defined(RTC_AB_NO_SLOTS)) && !defined(RTC_EXPERIMENT)
 #error "RTC_AB_* switches produce a wrong frame (timing experiments only): define RTC_EXPERIMENT as well"
 #endif
 
@@ -103,9 +102,6 @@ __device__ __forceinline__ float random_value(unsigned &s)
      * lies within r 2^-64 (< 2^-32) above r 2^-32, which cannot reach the next float rounding boundary but
      * does push an exact tie upward; r 2^-32 + r 2^-64 (one rounding) does the same.  Equal for all 2^32
      * values of r (checked exhaustively, tools/check_devmath.cpp). */
-#ifdef RTC_FAKE_RNG /* timing experiment only: not the reference's value */
-    return (float)r * 0x1p-32f;
-#endif
     const double d = (double)r * 0x1p-32;
     return (float)fma((double)r, 0x1p-64, d);
 }
@@ -165,39 +161,16 @@ __device__ __forceinline__ float rng_value_of_state(unsigned s)
 __device__ __forceinline__ float random_normal(unsigned &s)
 {
     float theta = (float)(2 * 3.14159265 * (double)random_value(s));
-#ifdef RTC_FAKE_BM /* timing experiment only: not the reference's value */
-    return __fsqrt_rn(-2.f * __logf(random_value(s))) * __cosf(theta);
-#endif
     float rho = (float)__builtin_sqrt(-2 * rtcmath::log((double)random_value(s)));
     return (float)((double)rho * rtcmath::cos((double)theta));
 }
-#ifndef RTC_BM_FALLBACK_SERIAL
-#define RTC_BM_FALLBACK_SERIAL 0
-#endif
-/* the exact restatement of three normals (the fallback of random_direction); inlined (out of line, with
- * RTC_BM_NOINLINE_FALLBACK, the chain kernel spills less but runs ~1.5% slower) */
-#ifdef RTC_BM_NOINLINE_FALLBACK
-__attribute__((noinline))
-#endif
+/* the exact restatement of three normals (the fallback of random_direction); inlined (out of line the chain kernel
+ * spilled less but ran ~1.5% slower; one normal at a time in a loop, no gain: round 4) */
 static __device__ __forceinline__ void random_normals_exact(unsigned &s, float v[3])
 {
-#if RTC_BM_FALLBACK_SERIAL
-    /* one normal at a time (a loop that is not unrolled): the rare fallback's live registers are one normal's, not
-     * three interleaved normals' -- they set the chain kernel's peak register pressure */
-    float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll 1
-    for (int k = 0; k < 3; ++k) {
-        const float n = random_normal(s);
-        a = k == 0 ? n : a;
-        b = k == 1 ? n : b;
-        c = k == 2 ? n : c;
-    }
-    v[0] = a, v[1] = b, v[2] = c;
-#else
     v[0] = random_normal(s);
     v[1] = random_normal(s);
     v[2] = random_normal(s);
-#endif
 }
 /* RandomDiretion (moremath.c:104-108), components drawn x, y, z.  The three normals take the certified fast
  * path (rtc_math.h bm_rho_fast / bm_normal_fast: table-driven log and cos, each float returned only when it
@@ -211,40 +184,24 @@ __device__ __forceinline__ V3 random_direction(unsigned &s, const rtcmath::BmLog
     (void)random_value(s), (void)random_value(s), (void)random_value(s);
     return normalized(V3{a, b, c + 1e-3f});
 #endif
-#ifndef RTC_EXACT_BM
     const unsigned s0 = s;
     float v[3];
     bool ok = true;
-#ifdef RTC_BM_SERIAL /* experiment: one normal at a time (fewer live registers, less ILP) */
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
     for (int c = 0; c < 3; ++c) {
         const float theta = (float)(2 * 3.14159265 * (double)random_value(s)); /* moremath.c:99 */
         float rho;
         ok = rtcmath::bm_rho_fast(random_value(s), rho, logTab) && ok;
         ok = rtcmath::bm_normal_fast(rho, theta, v[c], cosTab) && ok;
     }
-#ifndef RTC_AB_NO_BM_FALLBACK /* timing experiment only (the exact fallback's register cost): not the reference */
     if (__builtin_expect(!ok, 0)) {
-#ifdef RTC_DIAG_BMFALL /* diagnostic builds: the lanes that take the fallback, per wave slot (rtc_diag_itemlog) */
+#ifdef RTC_DIAG /* diagnostic builds: the lanes that take the fallback, per wave slot (rtc_diag_itemlog) */
         atomicAdd(&g_rtc_bmfall[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 65535u], 1u);
 #endif
         s = s0;
         random_normals_exact(s, v);
     }
-#else
-    (void)ok;
-    (void)s0;
-#endif
     return normalized(V3{v[0], v[1], v[2]});
-#else
-    float a = random_normal(s);
-    float b = random_normal(s);
-    float c = random_normal(s);
-    return normalized(V3{a, b, c});
-#endif
 }
 
 /* powf for the environment (raytracing.c:153,155): glibc 2.35's own powf algorithm, tables and
@@ -296,23 +253,6 @@ struct PowTablesLds {
     }
 };
 
-/* The certified Box-Muller tables (rtc_bm_tables.h) staged in LDS by a workgroup (call before its first __syncthreads;
- * 192 threads fill them): random_direction's six lookups per draw are then LDS reads instead of global loads, which a
- * hit's shading waited for on vmcnt behind the wave's older loads */
-struct BmTablesLds {
-    rtcmath::BmLogEntry log[128];
-    double cos[64][2];
-    __device__ __forceinline__ void fill(int tid)
-    {
-        if (tid < 128)
-            log[tid] = rtcmath::kBmLogTab[tid];
-        else if (tid < 192) {
-            cos[tid - 128][0] = rtcmath::kBmCosTab[tid - 128][0];
-            cos[tid - 128][1] = rtcmath::kBmCosTab[tid - 128][1];
-        }
-    }
-};
-
 /* getEnvironmentLight (raytracing.c:151-160) */
 /* fmax(0, v) as the reference's libm evaluates it (raytracing.c:155, double fmax of a float): NaN -> 0, v < 0
  * -> +0, otherwise v itself -- -0 included (x86-64 glibc returns its second operand for equal zeros) */
@@ -341,10 +281,7 @@ __device__ __forceinline__ V3 environment_t(V3 dir, const EnvParams &s)
     /* smoothstep's value is +0 .. 1 or NaN (never negative, never -0: clamp01 keeps -0 but (-0)^2 = +0) and the
      * exponent 0.35 is not special, so glibc's powf takes its positive-x path: that path alone, branch-free */
     const unsigned sa = __float_as_uint(skyArg);
-#ifndef RTC_SKY_UNIT
-#define RTC_SKY_UNIT 1
-#endif
-    if (RTC_SKY_UNIT && __all(sa - 0x00800000u <= 0x3f800000u - 0x00800000u)) /* every lane normal x in (0, 1]: main path */
+    if (__all(sa - 0x00800000u <= 0x3f800000u - 0x00800000u)) /* every lane normal x in (0, 1]: main path */
         skyGradientT = rtcmath::powf_sky_unit(skyArg, s.log2tab, s.exp2tab);
     else if (__any(sa != 0u))
         skyGradientT = rtcmath::powf_glibc_pos<true>(skyArg, 0.35f, s.log2tab, s.exp2tab);

@@ -95,8 +95,18 @@ struct Rccl {
     decltype(&ncclGroupStart) groupStart = nullptr;
     decltype(&ncclGroupEnd) groupEnd = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
+    decltype(&ncclCommCount) commCount = nullptr; /* (optional: what each communicator reports, rtc_last_multi_info) */
     bool ok = false;
 };
+
+/* What the last rtc_render_multi call of this thread ran on (rtc_last_multi_info): the path, and per
+ * communicator the rank count RCCL itself reports (ncclCommCount), so a caller can show that RCCL saw every device */
+struct MultiInfo {
+    int path = 0; /* 0: no call yet, 1: RCCL gather, 2: host rows (RTC_F_HOST_ROWS, no communicator) */
+    int devices = 0;
+    std::vector<int> commRanks;
+};
+thread_local MultiInfo g_multiInfo;
 
 const Rccl &rccl()
 {
@@ -113,6 +123,7 @@ const Rccl &rccl()
         x.groupStart = (decltype(x.groupStart))dlsym(h, "ncclGroupStart");
         x.groupEnd = (decltype(x.groupEnd))dlsym(h, "ncclGroupEnd");
         x.errorString = (decltype(x.errorString))dlsym(h, "ncclGetErrorString");
+        x.commCount = (decltype(x.commCount))dlsym(h, "ncclCommCount");
         x.ok = x.commInitAll && x.commDestroy && x.gather && x.groupStart && x.groupEnd && x.errorString;
         return x;
     }();
@@ -258,9 +269,13 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         return rc;
     if (numDevices > n)
         return rtc_fail(RTC_EINVAL, "rtc_render_multi: %d devices requested, %d present", numDevices, n);
-    if (d->flags & RTC_F_HOST_ROWS)
+    g_multiInfo = MultiInfo{};
+    g_multiInfo.devices = numDevices;
+    if (d->flags & RTC_F_HOST_ROWS) {
+        g_multiInfo.path = 2;
         return rtc_render_multi_host_rows(tris, triCount, spheres, sphereCount, scene, cam, d, numDevices, outImage,
                                           outAccum, stats, t0);
+    }
     const Rccl &R = rccl();
     if (!R.ok)
         return rtc_fail(RTC_ENODEV, "rtc_render_multi: RCCL (librccl.so.1) could not be loaded: %s", dlerror());
@@ -286,6 +301,13 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
                     (void)R.commDestroy(x);
         }
     } commGuard{R, comms};
+    g_multiInfo.path = 1;
+    for (int g = 0; g < G; ++g) { /* the size of the clique as each communicator sees it (-1: not reported) */
+        int c = -1;
+        if (!R.commCount || R.commCount(comms[g], &c) != ncclSuccess)
+            c = -1;
+        g_multiInfo.commRanks.push_back(c);
+    }
 
     /* device 0 also holds the gathered parts and the re-interleaved frame.  Declared before the parts (destroyed
      * after them): the parts' guard synchronises every stream first, so no gather or copy still in flight on an
@@ -303,6 +325,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         int rows = 0;
     };
     std::vector<Part> parts(G);
+    const float share = rtc_upload_hit_share(tris, triCount); /* the scheduling hint, estimated once for every device */
     Events evs;
     struct PartsGuard {
         std::vector<Part> &p;
@@ -322,7 +345,7 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
         RtcDeviceGuard dg(g);
         const RtcRenderDesc dg_desc = part_desc(d, g, G);
         p.rows = rtc_rows_selected(&dg_desc);
-        if (int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s))
+        if (int rc = rtc_scene_upload_with_share(tris, triCount, spheres, sphereCount, g, share, &p.s))
             return rc;
         HIP_TRY(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
         HIP_TRY(p.col.alloc(partPx * 3, g));
@@ -414,6 +437,18 @@ extern "C" int rtc_render_multi(const Triangle *tris, int triCount, const Sphere
     return 0;
 }
 
+extern "C" int rtc_last_multi_info(int *path, int *devices, int *commRanks, int maxComms)
+{
+    if (path)
+        *path = g_multiInfo.path;
+    if (devices)
+        *devices = g_multiInfo.devices;
+    const int n = (int)g_multiInfo.commRanks.size();
+    for (int i = 0; commRanks && i < n && i < maxComms; ++i)
+        commRanks[i] = g_multiInfo.commRanks[(size_t)i];
+    return n;
+}
+
 /* RTC_F_HOST_ROWS: no gather -- each device copies its compact rows straight into their places of the pinned host
  * frame (rtc_copy_rows_d2h_dma: host pitch G*W*3), over its own PCIe link, concurrently; the reference's threads
  * likewise write their rows into the shared image (main.c:84, :285-302). */
@@ -442,6 +477,7 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
         std::string err;
     };
     std::vector<Part> parts(G);
+    const float share = rtc_upload_hit_share(tris, triCount); /* the scheduling hint, estimated once for every device */
     Events evs;
     struct PartsGuard {
         std::vector<Part> &p;
@@ -460,7 +496,7 @@ int rtc_render_multi_host_rows(const Triangle *tris, int triCount, const Sphere 
         RtcDeviceGuard dg(g);
         const RtcRenderDesc dg_desc = part_desc(d, g, G);
         p.rows = rtc_rows_selected(&dg_desc);
-        if (int rc = rtc_scene_upload(tris, triCount, spheres, sphereCount, g, &p.s))
+        if (int rc = rtc_scene_upload_with_share(tris, triCount, spheres, sphereCount, g, share, &p.s))
             return rc;
         HIP_TRY(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
         HIP_TRY(p.col.alloc(partPx * 3 + 16, g));

@@ -27,12 +27,11 @@
 #include <cstring>
 #include <vector>
 #ifdef RTC_DIAG
-#define RTC_DIAG_BMFALL 1
 __device__ unsigned g_rtc_bmfall[65536]; /* Box-Muller exact fallbacks per wave slot (diagnostic builds) */
 #endif
 
 #include "../../include/rtc.h"
-#include "rtc_device.h"
+#include "rtc_layout.h"
 #include "rtc_internal.h"
 #include "rtc_hip_util.h"
 
@@ -87,703 +86,9 @@ extern "C" int rtc_device_count(int *count)
     return 0;
 }
 
-/* ---- device scene layout ------------------------------------------------------------------------- */
-#ifndef RTC_PF_ORDER
-#define RTC_PF_ORDER 0
-#endif
-#ifndef RTC_UNROLL
-#define RTC_UNROLL 2
-#endif
-constexpr int kUnroll = RTC_UNROLL; /* records per scalar-load batch; arrays are padded to a multiple of 8 */
+/* ---- device scene layout: rtc_layout.h; upload: rtc_scene.hip; probes: rtc_probe.hip ---------------------- */
+constexpr int kUnroll = 2; /* records per scalar-load batch; arrays are padded to a multiple of 8 */
 static_assert(8 % (2 * kUnroll) == 0 || kUnroll == 1, "padding assumes two batches divide 8");
-/* 64 B per triangle, read wave-uniformly by s_load_dwordx16: A, AB, AC, N (the reference's stored normal). */
-struct __attribute__((aligned(64))) DevTri {
-    float ax, ay, az, abx, aby, abz, acx, acy, acz, nx, ny, nz, pad0, pad1, pad2, pad3;
-};
-/* material, read only for the winning triangle */
-struct __attribute__((aligned(32))) DevMat {
-    float r, g, b, emission, smoothness, pad0, pad1, pad2;
-};
-struct __attribute__((aligned(16))) DevSphere {
-    float cx, cy, cz, radius, r, g, b, emission, smoothness, pad0, pad1, pad2;
-};
-/* Per-launch records for primary rays (bounce 0): every primary ray starts at the camera origin O, so all
- * the quantities rayTriangle derives from the ray are LINEAR in its direction d:
- *   nd = d.N,  det = AB.(d x AC) = d.Gd,  uu = s0.(d x AC) = d.Gu,  vv = d.q0
- * with s0 = O - A, q0 = s0 x AB, Gd = AC x AB, Gu = AC x s0 (raytracing.c:189-206).
- * DevPrimF drives an exact-safe FILTER: FMA dot products against these vectors plus per-triangle error
- * bounds (rtc_prep_primary derives them in double) reject a lane only when the reference's own float
- * arithmetic provably rejects it.  Surviving lanes run the reference arithmetic with DevPrimX (AB, AC, s0,
- * q0 and dot(AC, q0) computed once per launch with the reference's f32 ops: bit-exact).
- *
- * Orientation folding: a hit needs dst = dot(AC, q0) * invDet >= EPSILON > 0, so sign(det) must equal the
- * sign of dAC0 = dot(AC, q0) -- a per-triangle constant for primary rays.  The filter vectors are stored
- * pre-multiplied by sigma = sign(dAC0) (exact negation), which turns the per-lane sign normalisation into
- * nothing: a lane is a candidate iff  sigma*det~ >= c  and  min(sigma*u~, sigma*v~, sigma*w~) >= -m. */
-struct __attribute__((aligned(64))) DevPrimF { /* 64 B: one s_load_dwordx16 */
-    float nx, ny, nz, mnd;      /* N and the nd margin (-inf: the triangle can never be hit, skip it) */
-    float gdx, gdy, gdz, c;     /* sigma*Gd and the det threshold c = EPSILON - ed, rounded down */
-    float gux, guy, guz, negm;  /* sigma*Gu and -m (the combined edge margin, negated) */
-    float q0x, q0y, q0z, pad0;  /* sigma*q0 */
-};
-struct __attribute__((aligned(64))) DevPrimX {
-    float abx, aby, abz, acx, acy, acz, s0x, s0y, s0z, q0x, q0y, q0z, dac0, pad[3];
-};
-
-/* ---- triangle clusters for bounce rays (rtc_render_chain) -----------------------------------------------
- * The triangles are grouped into clusters of kClusterSize (spatial median splits, rtc_build_clusters); a
- * bounce ray skips a whole cluster when its half-line provably passes farther from the cluster's bounding
- * ball than any point rayTriangle could report.  Bound (SURVEY Appendix A arithmetic, unit roundoff
- * u = 2^-24): for a reported hit (|det| >= EPSILON, u, v in the triangle, dst >= EPSILON) the exact point
- * pos + dst*dir lies within
- *     eps = rho * (alpha + beta * S) + gamma * (S + E)
- * of the triangle, where rho >= |dir|, S >= |pos - A|, E = the cluster's longest AB / AC edge, and
- *     beta = F k 45 u E^2 / EPSILON,  alpha = F k 32 u E^3 / EPSILON,  k = 1 / (1 - 8 u E^2 rhoMax / EPSILON)
- * (forward error of the f32 cross / dot products over the Cramer solution, divided by |det| >= EPSILON;
- * safety factor F = 4; gamma covers the f32 evaluation of the cull test itself).  Clusters with
- * 8 u E^2 rhoMax / EPSILON >= 1/2, and rays with |dir|_1 > rhoMax, are never culled. */
-constexpr int kClusterSize = 8;
-constexpr int kChunkClusters = 32; /* clusters per chunk (one 32-bit cull mask per lane in rtc_render_chain) */
-constexpr float kClusterRhoMax = 4.f;
-constexpr float kClusterGamma = 2e-5f;
-struct __attribute__((aligned(32))) DevCluster {
-    float cx, cy, cz, r;          /* bounding ball (every vertex A, A+AB, A+AC of the cluster inside) */
-    float alpha, beta, gammaE, e; /* the eps terms above: alpha, beta, gamma*E (or +inf: never cull), E */
-};
-
-/* The scene's own events only order its two streams on one device (the caller's frame / geometry events keep their
- * flags): no system-scope fence when they are recorded (RTC_ORDER_FENCE 1 restores it) */
-#ifndef RTC_ORDER_FENCE
-#define RTC_ORDER_FENCE 0
-#endif
-constexpr unsigned kOrderEventFlags = hipEventDisableTiming | (RTC_ORDER_FENCE ? 0u : hipEventDisableSystemFence);
-/* An unjoined sky pass (RTC_F_OVERLAP) writes its launch's Color (and accumulator) rows: what it writes where */
-constexpr int kSkySlots = 8;
-#ifndef RTC_CHAIN_WGS_FULL
-#define RTC_CHAIN_WGS_FULL 3
-#endif
-#ifndef RTC_CULL_PRIO
-#define RTC_CULL_PRIO 0
-#endif
-/* Small shares of more pixels (the 1080p 1/4 share, 518 k px) run the tile cull at issue priority 3 as well: the next
- * share's cull then competes on equal terms with this share's geometry kernel (1/4 share 0.1205 -> 0.1170 ms; the 1/8
- * share measured no better that way, profiles/r05_cpq_ab_cull_priority.log) */
-#ifndef RTC_CULL_PRIO_MIN_PIXELS
-#define RTC_CULL_PRIO_MIN_PIXELS 400000
-#endif
-/* Wave priority of the geometry kernel (s_setprio): its waves are issued before the sky pass's on a shared SIMD.  A row
- * share's chain kernel runs ~3 pixels per wave; as its waves retire, sky waves fill their slots and the remaining chain
- * waves -- the share's critical path -- got a sixth of the issue: a wave's third and fourth pixels took 2-7x its first
- * (tools/wave_spread.py).  Round 5: 1080p 1/8 share 0.0757 -> 0.0697 ms, whole frames unchanged (the sky pass still
- * fills the chain kernel's idle slots); the tile cull at priority 3 too (RTC_CULL_PRIO) within noise of it
- * (profiles/r05_pr_ab_wave_priority.log) */
-#ifndef RTC_CHAIN_PRIO
-#define RTC_CHAIN_PRIO 3
-#endif
-/* RTC_GEO_HINT (experiment, round 5, not kept): the tile cull puts the pixels that took more than one window in the
- * previous launch's geometry kernel (a per-pixel byte the kernel sets) first in the item order -- the longest items
- * first.  A scheduling hint: any hint contents give the same frame.  Measured (profiles/r05_gh_ab_geo_hint.log): the
- * 1080p shares unchanged (consecutive pipelined shares already fill each other's tails), the whole frame's geometry
- * kernel -3 % at the same frame time, fsuzane +4 % */
-#ifndef RTC_GEO_HINT
-#define RTC_GEO_HINT 0
-#endif
-#ifndef RTC_GEO_CLASSES
-#define RTC_GEO_CLASSES 0
-#endif
-#ifndef RTC_CHAIN_WGS_HIT
-#define RTC_CHAIN_WGS_HIT 4 /* whole frames of scenes whose bounce-hit share (bounce_hit_share) exceeds RTC_WGS_HIT_SHARE */
-#endif
-#ifndef RTC_WGS_HIT_SHARE
-#define RTC_WGS_HIT_SHARE 0.15
-#endif
-
-/* rtc_render_chain's geometry-pixel sub-lists: kGeoLists counters, kGeoCountStride ints (one 128-B line) apart; a ring
- * of kGeoRing counter sets of kGeoSetInts ints (see RtcDeviceScene::geoCounts) */
-constexpr int kGeoLists = 16, kGeoCountStride = 32;
-/* rtc_render_chain's item counters (RTC_ITEM_COUNTERS > 0): counter x at geoCount[x * kGeoCountStride +
- * kItemCounterOffset] (the line of sub-list x's count, which only rtc_tile_cull updates), zeroed with the counts */
-#ifndef RTC_ITEM_COUNTERS
-#define RTC_ITEM_COUNTERS 0 /* 0: the workgroup's LDS counter (see rtc_render_chain) */
-#endif
-constexpr int kItemCounters = RTC_ITEM_COUNTERS, kItemCounterOffset = 16;
-static_assert(kItemCounters <= kGeoLists, "one item counter per sub-list line at most");
-constexpr int kGeoRing = 16, kGeoSetInts = kGeoLists * kGeoCountStride;
-static_assert(kGeoSetInts >= kGeoLists * kGeoCountStride, "a counter set holds every sub-list counter");
-struct SkyKey {
-    const void *colors, *accum;
-    float cam[13], env[14];
-    int dims[9];
-};
-struct RtcDeviceScene {
-    int device;
-    int cuCount; /* compute units of the device (the persistent chain kernel's workgroups are a multiple of it) */
-    int triCount, triPadded, sphereCount; /* triPadded: multiple of kUnroll, zero (never-hit) records */
-    int clusterCount;   /* ceil(triCount / kClusterSize) */
-    DevTri *clTris;     /* clusterCount * kClusterSize records in cluster order, pad0 = reference index (int) */
-    DevCluster *clusters;
-    DevCluster *chunks; /* chunkCount balls over kChunkClusters consecutive clusters */
-    int chunkCount;
-    DevTri *tris;
-    DevMat *mats;
-    DevSphere *spheres;
-    /* per-launch primary records, one copy per scratch slot (primStride records each), written by rtc_prep_primary:
-     * an overlapped launch's preparation (on the cull stream) may run while the previous frame's geometry kernel still
-     * reads its own copy */
-    DevPrimF *primF;
-    DevPrimX *primX;
-    size_t primStride;
-    /* per-launch scratch (rtc_tile_cull / rtc_order_blocks): the candidate bit-sets (maskWords u64 per 8x8
-     * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
-    unsigned char *scratch;
-    size_t scratchCap; /* bytes */
-    /* RTC_F_OVERLAP: launches cycle through kSkySlots slots of the scratch; skyPending[h]: a sky pass that reads
-     * slot h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends; skyKey[h]: the rows,
-     * camera and environment it writes; skySeq[h]: its enqueue order) */
-    int flip;
-    /* rtc_render_chain's sub-list counters: a ring of kGeoRing sets, set q % kGeoRing for the q-th split launch;
-     * each launch's tile cull zeroes the next launch's set, so a launch on the same stream as the previous one
-     * needs no rtc_prep_primary to clear its counters (cullStream: that stream) */
-    int *geoCounts;
-    unsigned char *tileHint; /* RTC_GEO_HINT: per pixel (tile * 64 + bit) of the last launches, 1 = several windows */
-    size_t tileHintCap;
-    unsigned long long geoSeq;
-    hipStream_t cullStream;
-    bool cullValid;
-    double hitShare;  /* bounce_hit_share at upload */
-    int chainWgsFull; /* rtc_render_chain workgroups per CU for whole frames */
-    /* rtc_prep_primary's records of slot h are for prepOrigin[h], written on prepStream[h] (prepValid[h]: they exist) */
-    bool prepValid[kSkySlots];
-    float prepOrigin[kSkySlots][3];
-    hipStream_t prepStream[kSkySlots];
-    /* RTC_F_OVERLAP launches prepare and cull on `cst` (a high-priority stream of the scene): the next frame's tile
-     * cull then runs while this frame's geometry kernel still runs, instead of after it on the launch stream.
-     * slotUsed[h]: an overlapped launch used slot h (its sky pass ends at evSkyDone[h], its launch-stream kernels at
-     * evGeoDone[h]: a later launch's cull waits for both before rewriting the slot) */
-    hipStream_t cst;
-    hipStream_t cst2; /* RTC_SHARE_CHAIN_CS: the second cull stream (odd slots) */
-    bool slotUsed[kSkySlots];
-    hipEvent_t evCullSync; /* the launch stream's position when the culls move to `cst` */
-    bool skyPending[kSkySlots];
-    SkyKey skyKey[kSkySlots];
-    unsigned long long skySeq[kSkySlots], skyCount; /* enqueue order of the sky passes (skySeq[h] of slot h's) */
-    hipEvent_t evSkyDone[kSkySlots], evGeoDone[kSkySlots];
-    hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
-    /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
-     * sample order at the kernel's end by the wave that rendered the pixel (grown on demand, <= kSampleBufBudget
-     * bytes) */
-    unsigned char *samples;
-    size_t samplesCap; /* bytes */
-    int maskWords;     /* ceil(triPadded / 64) */
-    unsigned long long *segSlots; /* per-launch partial segment counters */
-    /* the split launch runs the sky kernel on `side`, concurrently with the heavy-tile kernel */
-    hipStream_t side;
-    hipEvent_t evFork, evJoin;
-    /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
-    hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
-    /* caller's event (rtc_scene_set_geometry_event): recorded on the caller's stream once a launch's
-     * geometry-pixel kernels are enqueued (before the join with the sky pass); null: none */
-    hipEvent_t geoEvent;
-    bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
-    bool timed;  /* the last launch was a split launch that recorded them */
-};
-
-/* The share of diffuse bounce rays that hit the scene again, estimated at upload (host, a fixed-seed probe): rays from
- * area-weighted random points of the triangles, in directions normal + a random unit vector (the reference's diffuse
- * lobe, raytracing.c:276-279, without the specular part), tested against every triangle in double precision with the
- * reference's backface rule.  Only a scheduling hint (rtc_render_chain's workgroups per CU): it never changes a
- * frame.  Measured shares: fsuzane 0.21, rsuzanne 0.11, ultracomplex 0.019, complex 0.016, cube 0. */
-static double bounce_hit_share(const Triangle *t, int n)
-{
-    if (n <= 0)
-        return 0.0;
-    struct D3 { double x, y, z; };
-    const auto sub3 = [](D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; };
-    const auto dot3 = [](D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
-    const auto cross3 = [](D3 a, D3 b) { return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; };
-    const auto d3 = [](vec3 v) { return D3{v.x, v.y, v.z}; };
-    std::vector<double> cdf((size_t)n);
-    double total = 0.0;
-    for (int i = 0; i < n; ++i) {
-        const D3 c = cross3(sub3(d3(t[i].posB), d3(t[i].posA)), sub3(d3(t[i].posC), d3(t[i].posA)));
-        total += 0.5 * std::sqrt(dot3(c, c));
-        cdf[(size_t)i] = total;
-    }
-    if (!(total > 0.0))
-        return 0.0;
-    unsigned long long st = 0x9E3779B97F4A7C15ull;
-    const auto uni = [&]() { /* xorshift64*, [0, 1) */
-        st ^= st >> 12;
-        st ^= st << 25;
-        st ^= st >> 27;
-        return (double)((st * 0x2545F4914F6CDD1Dull) >> 11) * (1.0 / 9007199254740992.0);
-    };
-    /* ~4 M ray-triangle tests at most past 64 rays (a 1 M-triangle scene: 64 rays, ~0.3 s of upload) */
-    const int rays = (int)std::min<long long>(2048, std::max<long long>(64, 4000000LL / n));
-    int hits = 0;
-    for (int r = 0; r < rays; ++r) {
-        const int i = (int)(std::lower_bound(cdf.begin(), cdf.end(), uni() * total) - cdf.begin());
-        const Triangle &T = t[std::min(i, n - 1)];
-        double u = uni(), w = uni();
-        if (u + w > 1.0) {
-            u = 1.0 - u;
-            w = 1.0 - w;
-        }
-        const D3 A = d3(T.posA), AB = sub3(d3(T.posB), A), AC = sub3(d3(T.posC), A);
-        D3 nn = d3(T.normal);
-        const double nl = std::sqrt(dot3(nn, nn));
-        if (!(nl > 0.0))
-            continue;
-        nn = D3{nn.x / nl, nn.y / nl, nn.z / nl};
-        D3 q{0, 0, 0};
-        double ql = 0.0;
-        do { /* a uniform random unit vector (rejection from the cube) */
-            q = D3{2 * uni() - 1, 2 * uni() - 1, 2 * uni() - 1};
-            ql = dot3(q, q);
-        } while (ql > 1.0 || ql < 1e-12);
-        ql = std::sqrt(ql);
-        D3 dir{nn.x + q.x / ql, nn.y + q.y / ql, nn.z + q.z / ql};
-        const double dl = std::sqrt(dot3(dir, dir));
-        if (!(dl > 1e-9))
-            continue;
-        dir = D3{dir.x / dl, dir.y / dl, dir.z / dl};
-        const D3 P{A.x + u * AB.x + w * AC.x + 1e-4 * nn.x, A.y + u * AB.y + w * AC.y + 1e-4 * nn.y,
-                   A.z + u * AB.z + w * AC.z + 1e-4 * nn.z};
-        for (int j = 0; j < n; ++j) { /* rayTriangle's tests (raytracing.c:186-214), in double */
-            if (dot3(dir, d3(t[j].normal)) >= 0.0)
-                continue;
-            const D3 a = d3(t[j].posA), ab = sub3(d3(t[j].posB), a), ac = sub3(d3(t[j].posC), a);
-            const D3 h = cross3(dir, ac);
-            const double det = dot3(ab, h);
-            if (std::fabs(det) < 1e-12)
-                continue;
-            const D3 sv = sub3(P, a);
-            const double uu = dot3(sv, h) / det;
-            if (uu < 0.0 || uu > 1.0)
-                continue;
-            const D3 qv = cross3(sv, ab);
-            const double vv = dot3(dir, qv) / det;
-            if (vv < 0.0 || uu + vv > 1.0 || dot3(ac, qv) / det < 1e-3)
-                continue;
-            ++hits;
-            break;
-        }
-    }
-    return (double)hits / (double)rays;
-}
-
-static void pack_scene(const Triangle *tris, int triCount, const Sphere *sph, int sphCount, std::vector<DevTri> &dt,
-                       std::vector<DevMat> &dm, std::vector<DevSphere> &ds)
-{
-    const size_t padded = ((size_t)(triCount > 0 ? triCount : 0) + 7) / 8 * 8 + 8;
-    /* zero records are never hit: N = 0 makes dot(dir, N) >= 0 (or NaN, and then det is NaN too) */
-    dt.assign(padded, DevTri{});
-    dm.assign(padded, DevMat{});
-    for (int i = 0; i < triCount; ++i) {
-        const Triangle &t = tris[i];
-        DevTri &d = dt[i];
-        memset(&d, 0, sizeof d);
-        d.ax = t.posA.x;
-        d.ay = t.posA.y;
-        d.az = t.posA.z;
-        /* raytracing.c:191-192 minus(posB, posA), minus(posC, posA): same f32 ops */
-        d.abx = t.posB.x - t.posA.x;
-        d.aby = t.posB.y - t.posA.y;
-        d.abz = t.posB.z - t.posA.z;
-        d.acx = t.posC.x - t.posA.x;
-        d.acy = t.posC.y - t.posA.y;
-        d.acz = t.posC.z - t.posA.z;
-        d.nx = t.normal.x;
-        d.ny = t.normal.y;
-        d.nz = t.normal.z;
-        DevMat &m = dm[i];
-        memset(&m, 0, sizeof m);
-        m.r = t.mat.color.x;
-        m.g = t.mat.color.y;
-        m.b = t.mat.color.z;
-        m.emission = t.mat.emissionStrength;
-        m.smoothness = t.mat.smoothness;
-    }
-    ds.resize(sphCount > 0 ? sphCount : 1);
-    for (int i = 0; i < sphCount; ++i) {
-        DevSphere &d = ds[i];
-        memset(&d, 0, sizeof d);
-        d.cx = sph[i].pos.x;
-        d.cy = sph[i].pos.y;
-        d.cz = sph[i].pos.z;
-        d.radius = sph[i].r;
-        d.r = sph[i].mat.color.x;
-        d.g = sph[i].mat.color.y;
-        d.b = sph[i].mat.color.z;
-        d.emission = sph[i].mat.emissionStrength;
-        d.smoothness = sph[i].mat.smoothness;
-    }
-}
-
-/* Clusters of kClusterSize triangles: recursive splits of the centroids along their longest extent, each
- * split at a multiple of kClusterSize so that every leaf but the last is full (ceil(n / 8) clusters). */
-static void split_clusters(const std::vector<DevTri> &dt, std::vector<int> &idx, size_t lo, size_t hi)
-{
-    const size_t n = hi - lo;
-    if (n <= (size_t)kClusterSize)
-        return;
-    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-    auto centroid = [&](int i, int a) {
-        const DevTri &t = dt[i];
-        const double A[3] = {t.ax, t.ay, t.az}, B[3] = {t.abx, t.aby, t.abz}, C[3] = {t.acx, t.acy, t.acz};
-        return A[a] + (B[a] + C[a]) / 3.0;
-    };
-    for (size_t k = lo; k < hi; ++k)
-        for (int a = 0; a < 3; ++a) {
-            const double c = centroid(idx[k], a);
-            if (c == c) {
-                mn[a] = std::min(mn[a], c);
-                mx[a] = std::max(mx[a], c);
-            }
-        }
-    int axis = 0;
-    for (int a = 1; a < 3; ++a)
-        if (mx[a] - mn[a] > mx[axis] - mn[axis])
-            axis = a;
-    std::stable_sort(idx.begin() + lo, idx.begin() + hi, [&](int p, int q) {
-        const double cp = centroid(p, axis), cq = centroid(q, axis);
-        return (cp == cp ? cp : 1e300) < (cq == cq ? cq : 1e300);
-    });
-    const size_t leaves = (n + kClusterSize - 1) / kClusterSize;
-    const size_t mid = lo + (leaves + 1) / 2 * kClusterSize;
-    split_clusters(dt, idx, lo, mid);
-    split_clusters(dt, idx, mid, hi);
-}
-
-/* Bounding ball and cull margins (DevCluster) of the records ct[first, first + count) whose index (pad0) is
- * >= 0: the ball holds every vertex A, A + AB, A + AC; E is the longest AB / AC edge. */
-static DevCluster ball_of(const std::vector<DevTri> &ct, size_t first, size_t count)
-{
-    const double u = 0x1p-24, eps = 0.001; /* |det| >= 0.001f > 0.001 for every reported hit */
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, E = 0.0;
-    bool finite = true;
-    int n = 0;
-    auto real = [&](const DevTri &r) {
-        int i;
-        memcpy(&i, &r.pad0, sizeof i);
-        return i >= 0;
-    };
-    for (size_t j = first; j < first + count; ++j) {
-        const DevTri &r = ct[j];
-        if (!real(r))
-            continue;
-        ++n;
-        const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
-        for (int a = 0; a < 3; ++a) {
-            const double v[3] = {A[a], A[a] + B[a], A[a] + C[a]};
-            for (double x : v) {
-                finite = finite && std::isfinite(x);
-                lo[a] = std::min(lo[a], x);
-                hi[a] = std::max(hi[a], x);
-            }
-        }
-        E = std::max(E, std::max(std::sqrt(B[0] * B[0] + B[1] * B[1] + B[2] * B[2]),
-                                 std::sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2])));
-    }
-    DevCluster k{};
-    const double ctr[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
-    k.cx = n ? (float)ctr[0] : 0.f;
-    k.cy = n ? (float)ctr[1] : 0.f;
-    k.cz = n ? (float)ctr[2] : 0.f;
-    double R = 0.0;
-    for (size_t j = first; j < first + count; ++j) { /* radius about the rounded (float) centre */
-        const DevTri &r = ct[j];
-        if (!real(r))
-            continue;
-        const double A[3] = {r.ax, r.ay, r.az}, B[3] = {r.abx, r.aby, r.abz}, C[3] = {r.acx, r.acy, r.acz};
-        const double K[3] = {k.cx, k.cy, k.cz};
-        for (int w = 0; w < 3; ++w) {
-            double d2 = 0.0;
-            for (int a = 0; a < 3; ++a) {
-                const double x = A[a] + (w == 1 ? B[a] : w == 2 ? C[a] : 0.0) - K[a];
-                d2 += x * x;
-            }
-            R = std::max(R, std::sqrt(d2));
-        }
-    }
-    const double F = 4.0, edRatio = 8.0 * u * E * E * kClusterRhoMax / eps;
-    k.r = std::nextafter((float)(R * (1.0 + 1e-9)), INFINITY);
-    k.e = (float)E;
-    if (!finite || n == 0 || !(edRatio < 0.5) || !(k.r < 1e18f)) {
-        k.alpha = INFINITY; /* never culled */
-        k.beta = k.gammaE = 0.f;
-        return k;
-    }
-    const double kk = 1.0 / (1.0 - edRatio);
-    k.alpha = std::nextafter((float)(F * kk * 32.0 * u * E * E * E / eps), INFINITY);
-    k.beta = std::nextafter((float)(F * kk * 45.0 * u * E * E / eps), INFINITY);
-    k.gammaE = std::nextafter((float)(kClusterGamma * E), INFINITY);
-    return k;
-}
-
-/* A triangle whose stored normal N points along its geometric normal G' = AB x AC closely enough that, for every
- * ray of |dir|_1 <= kClusterRhoMax, rayTriangle's backface test (dot(dir, N) < 0, raytracing.c:189) forces
- * det = dot(AB, dir x AC) > -EPSILON (raytracing.c:195): then a hit needs det >= EPSILON, and since
- * dst = dot(AC, q) / det (q = (pos - A) x AB, raytracing.c:202-206) must be >= EPSILON, dot(AC, q) > 0.  For a
- * ray origin where the reference's own f32 dot(AC, q) is <= 0 (pos on or behind the plane), the triangle cannot
- * be hit from there in any direction (rtc_render_chain's first bounces).  Bound: with N = a G'/|G'| + e (e
- * orthogonal), fl(dot(dir, N)) < 0 gives dir.G'/|G'| < rho (3.01u |N|_inf + |e|) / a, and |det + dir.G'| <=
- * 5.1u |AB|_1 |AC|_1 rho; aligned when rho times their sum, with a factor 2, stays below EPSILON. */
-static bool aligned_normal(const DevTri &r)
-{
-    const double u = 0x1p-24;
-    const double AB[3] = {r.abx, r.aby, r.abz}, AC[3] = {r.acx, r.acy, r.acz}, N[3] = {r.nx, r.ny, r.nz};
-    const double G[3] = {AB[1] * AC[2] - AB[2] * AC[1], AB[2] * AC[0] - AB[0] * AC[2], AB[0] * AC[1] - AB[1] * AC[0]};
-    const double g = std::sqrt(G[0] * G[0] + G[1] * G[1] + G[2] * G[2]);
-    if (!(g > 0.0) || !std::isfinite(g))
-        return false;
-    const double a = (N[0] * G[0] + N[1] * G[1] + N[2] * G[2]) / g;
-    if (!(a > 0.0))
-        return false;
-    const double e[3] = {N[0] - a * G[0] / g, N[1] - a * G[1] / g, N[2] - a * G[2] / g};
-    const double en = std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]) + 1e-12 * (std::fabs(N[0]) + std::fabs(N[1]) + std::fabs(N[2]));
-    const double ninf = std::max(std::fabs(N[0]), std::max(std::fabs(N[1]), std::fabs(N[2])));
-    const double n1 = std::fabs(AB[0]) + std::fabs(AB[1]) + std::fabs(AB[2]), c1 = std::fabs(AC[0]) + std::fabs(AC[1]) + std::fabs(AC[2]);
-    const double K = g * (3.01 * u * ninf + en) / a + 5.1 * u * n1 * c1;
-    return std::isfinite(K) && 2.0 * kClusterRhoMax * K < 0.001;
-}
-
-/* ct: the records in cluster order (pad0 = reference index, -1 for padding), cl: one ball per cluster of
- * kClusterSize, ch: one ball per chunk of kChunkClusters consecutive clusters (a subtree of the median split:
- * the chain kernel's first culling level for scenes of more than one chunk) */
-static void rtc_build_clusters(const std::vector<DevTri> &dt, int triCount, std::vector<DevTri> &ct,
-                               std::vector<DevCluster> &cl, std::vector<DevCluster> &ch)
-{
-    const int nc = (triCount + kClusterSize - 1) / kClusterSize;
-    std::vector<int> idx(triCount);
-    for (int i = 0; i < triCount; ++i)
-        idx[i] = i;
-    split_clusters(dt, idx, 0, (size_t)triCount);
-    ct.assign((size_t)nc * kClusterSize, DevTri{});
-    cl.assign((size_t)(nc > 0 ? nc : 1), DevCluster{});
-    for (int c = 0; c < nc; ++c) {
-        const int n = std::min(kClusterSize, triCount - c * kClusterSize);
-        for (int j = 0; j < kClusterSize; ++j) {
-            DevTri &r = ct[(size_t)c * kClusterSize + j];
-            if (j >= n) { /* zero record: never hit; index -1 */
-                const int none = -1;
-                memcpy(&r.pad0, &none, sizeof none);
-                continue;
-            }
-            const int i = idx[(size_t)c * kClusterSize + j];
-            r = dt[i];
-            memcpy(&r.pad0, &i, sizeof i);
-            const int al = aligned_normal(r) ? 1 : 0;
-            memcpy(&r.pad1, &al, sizeof al);
-        }
-        cl[c] = ball_of(ct, (size_t)c * kClusterSize, kClusterSize);
-    }
-    const int nch = (nc + kChunkClusters - 1) / kChunkClusters;
-    ch.assign((size_t)(nch > 0 ? nch : 1), DevCluster{});
-    for (int h = 0; h < nch; ++h) {
-        const size_t c0 = (size_t)h * kChunkClusters, c1 = std::min<size_t>((size_t)nc, c0 + kChunkClusters);
-        ch[h] = ball_of(ct, c0 * kClusterSize, (c1 - c0) * kClusterSize);
-    }
-}
-
-extern "C" int rtc_bounce_hit_share(const Triangle *tris, int triCount, float *share)
-{
-    if (!share || triCount < 0 || (triCount > 0 && !tris))
-        return rtc_fail(RTC_EINVAL, "rtc_bounce_hit_share: bad argument");
-    *share = (float)bounce_hit_share(tris, triCount);
-    return 0;
-}
-
-extern "C" int rtc_scene_chain_wgs(const RtcDeviceScene *s)
-{
-    if (!s)
-        return rtc_fail(RTC_EINVAL, "rtc_scene_chain_wgs: null scene");
-    return s->chainWgsFull;
-}
-
-extern "C" int rtc_scene_upload(const Triangle *tris, int triCount, const Sphere *spheres, int sphereCount, int device,
-                                RtcDeviceScene **out)
-{
-    if (!out || triCount < 0 || sphereCount < 0 || (triCount > 0 && !tris) || (sphereCount > 0 && !spheres))
-        return rtc_fail(RTC_EINVAL, "rtc_scene_upload: bad argument");
-    *out = nullptr;
-    int n = 0;
-    int rc = rtc_device_count(&n);
-    if (rc)
-        return rc;
-    if (device < 0)
-        HIP_TRY(hipGetDevice(&device));
-    if (device >= n)
-        return rtc_fail(RTC_EINVAL, "device %d out of range (%d devices)", device, n);
-    RtcDeviceGuard guard(device);
-    if (!guard.ok())
-        return rtc_fail(RTC_ENODEV, "rtc_scene_upload: cannot select device %d", device);
-    std::vector<DevTri> dt;
-    std::vector<DevMat> dm;
-    std::vector<DevSphere> ds;
-    pack_scene(tris, triCount, spheres, sphereCount, dt, dm, ds);
-    std::vector<DevTri> ct;
-    std::vector<DevCluster> cl, ch;
-    rtc_build_clusters(dt, triCount, ct, cl, ch);
-    if (ct.empty())
-        ct.assign(1, DevTri{});
-    RtcDeviceScene *s = new RtcDeviceScene();
-    s->device = device;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
-        cus = 256; /* MI355X */
-    s->cuCount = cus;
-    s->triCount = triCount;
-    s->triPadded = (triCount + 7) / 8 * 8; /* whole pairs of batches; arrays hold 8 more records for prefetch */
-    s->sphereCount = sphereCount;
-    s->maskWords = (s->triPadded + 63) / 64;
-    s->clusterCount = (triCount + kClusterSize - 1) / kClusterSize;
-    s->chunkCount = (s->clusterCount + kChunkClusters - 1) / kChunkClusters;
-    /* whole frames of scenes whose bounce rays often hit again (fsuzane) run 4 chain workgroups per CU: their frame is
-     * nearly all geometry kernel, which then has the registers the co-resident sky waves would use (round 5, 1080p x64:
-     * fsuzane 1.25 -> 1.16 ms per frame; ultracomplex 0.348 -> 0.379, complex 4K 1.22 -> 1.34, so 3 stays the default,
-     * profiles/r05_w4_ab_chain_wgs.log) */
-    s->hitShare = bounce_hit_share(tris, triCount);
-    s->chainWgsFull = s->hitShare > RTC_WGS_HIT_SHARE ? RTC_CHAIN_WGS_HIT : RTC_CHAIN_WGS_FULL;
-    hipError_t e = hipMalloc(&s->tris, dt.size() * sizeof(DevTri));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->clTris, ct.size() * sizeof(DevTri));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->clusters, cl.size() * sizeof(DevCluster));
-    if (e == hipSuccess)
-        e = hipMemcpy(s->clTris, ct.data(), ct.size() * sizeof(DevTri), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(s->clusters, cl.data(), cl.size() * sizeof(DevCluster), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMalloc(&s->chunks, ch.size() * sizeof(DevCluster));
-    if (e == hipSuccess)
-        e = hipMemcpy(s->chunks, ch.data(), ch.size() * sizeof(DevCluster), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMalloc(&s->mats, dm.size() * sizeof(DevMat));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->spheres, ds.size() * sizeof(DevSphere));
-    s->primStride = dt.size();
-    if (e == hipSuccess)
-        e = hipMalloc(&s->primF, kSkySlots * dt.size() * sizeof(DevPrimF));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->primX, kSkySlots * dt.size() * sizeof(DevPrimX));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->segSlots, 256 * 16 * sizeof(unsigned long long));
-    if (e == hipSuccess) /* kept zero between launches by rtc_reduce_segments */
-        e = hipMemset(s->segSlots, 0, 256 * 16 * sizeof(unsigned long long));
-    if (e == hipSuccess)
-        e = hipMalloc(&s->geoCounts, kGeoRing * kGeoSetInts * sizeof(int));
-    if (e == hipSuccess)
-        e = hipMemset(s->geoCounts, 0, kGeoRing * kGeoSetInts * sizeof(int));
-    if (e == hipSuccess)
-        e = hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(s->mats, dm.data(), dm.size() * sizeof(DevMat), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(s->spheres, ds.data(), ds.size() * sizeof(DevSphere), hipMemcpyHostToDevice);
-    int leastPrio = 0, greatestPrio = 0;
-    if (e == hipSuccess)
-        e = hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio);
-    if (e == hipSuccess) /* the sky tiles yield to the heavy tiles */
-        e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, leastPrio);
-    if (e == hipSuccess) /* the next frame's cull goes first wherever a CU frees up */
-        e = hipStreamCreateWithPriority(&s->cst, hipStreamNonBlocking, greatestPrio);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evCullSync, kOrderEventFlags);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evFork, kOrderEventFlags);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&s->evJoin, kOrderEventFlags);
-    for (int h = 0; h < kSkySlots; ++h)
-        if (e == hipSuccess)
-            e = hipEventCreateWithFlags(&s->evSkyDone[h], kOrderEventFlags);
-    for (int h = 0; h < kSkySlots; ++h)
-        if (e == hipSuccess)
-            e = hipEventCreateWithFlags(&s->evGeoDone[h], kOrderEventFlags);
-    for (hipEvent_t *ev : {&s->evHeavy0, &s->evHeavy1, &s->evSky0, &s->evSky1})
-        if (e == hipSuccess)
-            e = hipEventCreate(ev);
-    if (e != hipSuccess) {
-        rtc_scene_release(s);
-        return rtc_fail(-(int)e, "scene upload failed: %s", hipGetErrorString(e));
-    }
-    *out = s;
-    return 0;
-}
-
-extern "C" int rtc_scene_release(RtcDeviceScene *s)
-{
-    if (!s)
-        return 0;
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    (void)hipSetDevice(s->device);
-    if (s->side) /* an unjoined sky pass (RTC_F_OVERLAP) may still read the scratch */
-        (void)hipStreamSynchronize(s->side);
-    if (s->cst)
-        (void)hipStreamSynchronize(s->cst);
-    if (s->cst2)
-        (void)hipStreamSynchronize(s->cst2);
-    if (s->tris)
-        (void)hipFree(s->tris);
-    if (s->clTris)
-        (void)hipFree(s->clTris);
-    if (s->clusters)
-        (void)hipFree(s->clusters);
-    if (s->chunks)
-        (void)hipFree(s->chunks);
-    if (s->mats)
-        (void)hipFree(s->mats);
-    if (s->spheres)
-        (void)hipFree(s->spheres);
-    if (s->primF)
-        (void)hipFree(s->primF);
-    if (s->primX)
-        (void)hipFree(s->primX);
-    if (s->scratch)
-        (void)hipFree(s->scratch);
-    if (s->samples)
-        (void)hipFree(s->samples);
-    if (s->segSlots)
-        (void)hipFree(s->segSlots);
-    if (s->geoCounts)
-        (void)hipFree(s->geoCounts);
-    if (s->tileHint)
-        (void)hipFree(s->tileHint);
-    if (s->evFork)
-        (void)hipEventDestroy(s->evFork);
-    if (s->evJoin)
-        (void)hipEventDestroy(s->evJoin);
-    for (hipEvent_t ev : {s->evHeavy0, s->evHeavy1, s->evSky0, s->evSky1, s->evCullSync})
-        if (ev)
-            (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : s->evSkyDone)
-        if (ev)
-            (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : s->evGeoDone)
-        if (ev)
-            (void)hipEventDestroy(ev);
-    if (s->side)
-        (void)hipStreamDestroy(s->side);
-    if (s->cst)
-        (void)hipStreamDestroy(s->cst);
-    if (s->cst2)
-        (void)hipStreamDestroy(s->cst2);
-    if (cur >= 0)
-        (void)hipSetDevice(cur);
-    delete s;
-    return 0;
-}
-
-extern "C" int rtc_rows_selected(const RtcRenderDesc *d)
-{
-    if (!d || d->rowStride <= 0 || d->rowStart < 0 || d->rowStart >= d->height || d->height <= 0 || d->rowBand < 0)
-        return 0;
-    /* bands of B rows (rowBand, rtc.h): the full bands' rows, plus the last band's rows inside the frame */
-    const long long B = d->rowBand > 1 ? d->rowBand : 1, step = (long long)d->rowStride * B;
-    const long long nb = (d->height - d->rowStart + step - 1) / step, last = d->rowStart + (nb - 1) * step;
-    return (int)((nb - 1) * B + std::min<long long>(B, d->height - last));
-}
 
 /* ---- the render kernel ---------------------------------------------------------------------------- */
 /* one deferred sample: radiance * (1/spp), 12 B (stored and read as 3 dwords) */
@@ -818,9 +123,7 @@ struct RenderParams {
     int *__restrict__ geoCountNext; /* the next split launch's counters, zeroed by this launch's rtc_tile_cull */
     int *__restrict__ geoList;
     int geoCap; /* entries per sub-list */
-    int cullPrio; /* rtc_tile_cull's waves at issue priority 3 (RTC_CULL_PRIO_MIN_PIXELS) */
-    unsigned char *tileHint; /* RTC_GEO_HINT (null: none), per pixel tile * 64 + bit: read and cleared by rtc_tile_cull,
-                              * set by rtc_render_chain for pixels of more than one window */
+    int cullPrio; /* rtc_tile_cull's waves at issue priority 3 (kCullPrioMinPixels) */
     int blocksX; /* 16x16 blocks per row of the launch */
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
@@ -842,12 +145,9 @@ struct RenderParams {
 };
 
 /* Data a kernel only reads (written by earlier kernels of the launch) at a wave-uniform address, read through
- * the constant address space so that the compiler issues scalar loads (RTC_SMEM): they return on lgkmcnt,
+ * the constant address space so that the compiler issues scalar loads: they return on lgkmcnt,
  * so waiting for one does not also wait for the wave's earlier sample-slot stores to be acknowledged, as a
  * vector load's vmcnt wait does on gfx9 (loads and stores share vmcnt). */
-#ifndef RTC_SMEM
-#define RTC_SMEM 1
-#endif
 template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *kconst(const T *p)
 {
     return (const __attribute__((address_space(4))) T *)p;
@@ -863,15 +163,10 @@ template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
         ((unsigned *)&v)[k] = q[k];
     return v;
 }
-#if RTC_SMEM
 #define KCONST(p) kconst(p)
 #define KLOAD(p, i) kload(p, i)
-#else
-#define KCONST(p) (p)
-#define KLOAD(p, i) ((p)[i])
-#endif
 
-/* A RenderParams field of the launch, re-read from the kernarg segment where it is used (RTC_KARG; values, and pointers
+/* A RenderParams field of the launch, re-read from the kernarg segment where it is used (KARG; values, and pointers
  * read through KCONST / KLOAD / gload only -- a pointer loaded this way has no known address space, so a plain vector
  * access through it would be a flat one, whose wait covers lgkmcnt too): the kernel's one
  * argument is RenderParams at offset 0 of that segment.  The segment pointer is laundered through an empty asm at every
@@ -879,9 +174,6 @@ template <typename T> __device__ __forceinline__ T kload(const T *p, int i)
  * between uses.  rtc_render_chain keeps ~60 SGPRs of launch constants (camera, environment, dimensions, pointers)
  * otherwise, and spilled 155 SGPRs to VGPR lanes (v_writelane / v_readlane in its loops).  For fields
  * read once per item, window or escaped bounce: a scalar-cache hit against a register that would have been spilled. */
-#ifndef RTC_KARG
-#define RTC_KARG 1
-#endif
 /* 0 in a vector register the compiler cannot see through: a wave-uniform address plus vzero() is read by a vector load
  * (waited for by vmcnt, in order) instead of a scalar load */
 __device__ __forceinline__ int vzero()
@@ -910,11 +202,17 @@ template <typename T> __device__ __forceinline__ T karg_at(size_t off)
         ((unsigned *)&v)[k] = q[k];
     return v;
 }
-#if RTC_KARG
-#define KARG(field) karg_at<decltype(RenderParams::field)>(offsetof(RenderParams, field))
-#else
-#define KARG(field) (P.field)
-#endif
+/* Contract: KARG(field) names `P`, which must be the calling kernel's one RenderParams argument -- every
+ * kernel that uses KARG, directly or through a helper, is declared `kernel(RenderParams P, ...)` with P first, at
+ * kernarg offset 0 (rtc_tile_cull, rtc_render_chain), and a helper that uses it takes `const RenderParams &P`.
+ * karg_field refuses any other `P` at compile time. */
+template <typename PT, typename T> __device__ __forceinline__ T karg_field(size_t off)
+{
+    static_assert(std::is_same<typename std::decay<PT>::type, RenderParams>::value,
+                  "KARG reads the kernel's RenderParams argument: P must be it");
+    return karg_at<T>(off);
+}
+#define KARG(field) karg_field<decltype(P), decltype(RenderParams::field)>(offsetof(RenderParams, field))
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 
@@ -991,11 +289,8 @@ __global__ __launch_bounds__(64) void rtc_prep_primary(const DevTri *__restrict_
                                                         int *__restrict__ geoCount)
 {
     const int t = blockIdx.x * 64 + threadIdx.x;
-    if (geoCount && blockIdx.x == 0 && threadIdx.x < kGeoLists) { /* the launch's geometry sub-lists start empty */
+    if (geoCount && blockIdx.x == 0 && threadIdx.x < kGeoLists) /* the launch's geometry sub-lists start empty */
         geoCount[threadIdx.x * kGeoCountStride] = 0;
-        if (threadIdx.x < kItemCounters)
-            geoCount[threadIdx.x * kGeoCountStride + kItemCounterOffset] = 0;
-    }
     if (t >= triCount)
         return;
     const DevTri T = tris[t];
@@ -1130,24 +425,6 @@ __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, C
     for (int k = 0; k < kUnroll; ++k)
         A[k] = rec[k];
     for (int t0 = 0; t0 < P.triPadded; t0 += 2 * kUnroll, rec += 2 * kUnroll) {
-#if RTC_PF_ORDER
-        /* SMEM returns out of order, so the first use of a batch waits for every scalar load in flight:
-         * issue the next batch only after the current batch has been touched */
-        primary_test(P, dir, A[0], t0, base, c);
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k)
-            B[k] = rec[kUnroll + k];
-#pragma unroll
-        for (int k = 1; k < kUnroll; ++k)
-            primary_test(P, dir, A[k], t0 + k, base, c);
-        primary_test(P, dir, B[0], t0 + kUnroll, base, c);
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k)
-            A[k] = rec[2 * kUnroll + k];
-#pragma unroll
-        for (int k = 1; k < kUnroll; ++k)
-            primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
-#else
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
             B[k] = rec[kUnroll + k];
@@ -1160,7 +437,6 @@ __device__ __forceinline__ void closest_primary(const RenderParams &P, V3 dir, C
 #pragma unroll
         for (int k = 0; k < kUnroll; ++k)
             primary_test(P, dir, B[k], t0 + kUnroll + k, base, c);
-#endif
     }
 }
 
@@ -1245,9 +521,6 @@ __device__ __forceinline__ void general_test(V3 pos, V3 dir, const DevTri &R, in
 /* Scenes up to kLdsTris triangles keep their general-path records in LDS (one copy per workgroup, loaded at
  * kernel start): the general loop then reads them as broadcast ds_read_b128 instead of scalar loads that
  * compete for the scalar cache with the primary records. */
-#ifndef RTC_GEN_LDS
-#define RTC_GEN_LDS 1
-#endif
 constexpr int kLdsTris = 256;
 
 __device__ __forceinline__ void closest_general_lds(const DevTri *__restrict__ lds, int Tp, V3 pos, V3 dir,
@@ -1260,13 +533,9 @@ __device__ __forceinline__ void closest_general_lds(const DevTri *__restrict__ l
     }
 }
 
-#ifndef RTC_GEN_PF
-#define RTC_GEN_PF 1
-#endif
 __device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V3 dir, Closest &c, int base)
 {
     const int Tp = P.triPadded;
-#if RTC_GEN_PF
     /* two alternating scalar-load batches, as closest_primary: the next records are in flight while the
      * current ones are tested (the arrays carry 8 spare records) */
     const DevTri *rec = P.tris;
@@ -1288,17 +557,6 @@ __device__ __forceinline__ void closest_general(const RenderParams &P, V3 pos, V
         for (int k = 0; k < kUnroll; ++k)
             general_test(pos, dir, B[k], base + t0 + kUnroll + k, c);
     }
-#else
-    for (int t0 = 0; t0 < Tp; t0 += kUnroll) {
-        DevTri RR[kUnroll];
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k)
-            RR[k] = P.tris[t0 + k];
-#pragma unroll
-        for (int k = 0; k < kUnroll; ++k)
-            general_test(pos, dir, RR[k], base + t0 + k, c);
-    }
-#endif
 }
 
 /* calculateRayCollision (raytracing.c:216-240): spheres first (only if !trianglesOnly), then triangles
@@ -1587,14 +845,8 @@ __device__ bool tile_prunes(const TileCone &K, const DevPrimF &F)
  * so rtc_tile_cull's level 1 tests only its survivors, and a block whose superblock keeps none (the sky of a frame)
  * skips its own double-precision cone.  Same candidate lists bit for bit (each level only removes triangles the
  * per-pixel filter rejects for every pixel of the rectangle). */
-#ifndef RTC_CULL_SUPER
-#define RTC_CULL_SUPER 1
-#endif
 constexpr int kSuperBlocks = 4;
-#ifndef RTC_SUPER_CULL_PIXELS
-#define RTC_SUPER_CULL_PIXELS 400000
-#endif
-constexpr size_t kSuperCullPixels = RTC_SUPER_CULL_PIXELS; /* launches of more pixels run level 0 */
+constexpr size_t kSuperCullPixels = 400000; /* launches of more pixels run level 0 */
 __global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned long long *__restrict__ superMask)
 {
     const int sx = blockIdx.x, sy = blockIdx.y, lane = threadIdx.x;
@@ -1614,12 +866,8 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
                                                        unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
                                                        unsigned long long *__restrict__ pixMask)
 {
-#if RTC_CULL_PRIO > 0
-    __builtin_amdgcn_s_setprio(RTC_CULL_PRIO);
-#else
     if (KARG(cullPrio)) /* (RenderParams::cullPrio) */
         __builtin_amdgcn_s_setprio(3);
-#endif
     __shared__ unsigned wgWeight, wgAny;
     extern __shared__ unsigned long long sBlockCand[]; /* maskWords: the block's 16x16 prefilter survivors */
     CSTAMP(c0);
@@ -1629,14 +877,8 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     }
     const int bx = blockIdx.x, by = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (P.geoCountNext && bx == 0 && by == 0 && threadIdx.x < kGeoLists) { /* the next split launch's sub-lists */
+    if (P.geoCountNext && bx == 0 && by == 0 && threadIdx.x < kGeoLists) /* the next split launch's sub-lists */
         P.geoCountNext[threadIdx.x * kGeoCountStride] = 0;
-        if (threadIdx.x < kItemCounters) /* and its geometry kernel's item counters */
-            P.geoCountNext[threadIdx.x * kGeoCountStride + kItemCounterOffset] = 0;
-    }
-#ifndef RTC_TILE_PREFILTER
-#define RTC_TILE_PREFILTER 1
-#endif
     /* level 1: the prefilter over the workgroup's 16x16 pixels (a superset of each tile's direction range, so
      * a triangle it prunes fails for every pixel of the four tiles); the waves share the mask words */
     __syncthreads();
@@ -1652,7 +894,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
             const int ti = w * 64 + lane;
             const unsigned long long sw = sup ? KCONST(sup)[w] : ~0ull;
             const bool maybe = ((sw >> lane) & 1ull) && ti < P.triPadded &&
-                               (!RTC_TILE_PREFILTER || !KB.ok || !tile_prunes(KB, P.primF[ti]));
+                               (!KB.ok || !tile_prunes(KB, P.primF[ti]));
             const unsigned long long m = __ballot(maybe);
             if (lane == 0) {
                 sBlockCand[w] = m;
@@ -1683,7 +925,6 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 #endif
     const PixelRay px = pixel_ray(P, bx, by);
     bool anyCand = false;
-    int nCand = 0; /* the tile's candidates (RTC_GEO_CLASSES) */
     /* level 2: the tile's own prefilter on the block's survivors, then the per-pixel filter */
     const TileCone K = tile_cone(P, tile % (int)(gridDim.x * 2), tile / (int)(gridDim.x * 2));
     for (int w = 0; w < P.maskWords; ++w) {
@@ -1691,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         const int ti = w * 64 + lane;
         const unsigned long long bc = sBlockCand[w];
         CSTAMP(c2);
-        const bool maybe = ((bc >> lane) & 1ull) && (!RTC_TILE_PREFILTER || !K.ok || !tile_prunes(K, P.primF[ti]));
+        const bool maybe = ((bc >> lane) & 1ull) && (!K.ok || !tile_prunes(K, P.primF[ti]));
         unsigned long long todo = bc ? __ballot(maybe) : 0ull;
         unsigned long long bits = 0;
         CSTAMP(c3);
@@ -1714,7 +955,6 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
 #endif
         if (lane == 0)
             out[w] = bits;
-        nCand += __popcll(bits);
     }
     /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
      * non-empty candidate list exactly when its weight is > 0 */
@@ -1735,26 +975,7 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
             if (((gb >> lane) & 1ull) && base + __popcll(gb) <= P.geoCap)
                 P.geoList[(size_t)l * P.geoCap + base + __popcll(gb & ((1ull << lane) - 1ull))] = tile * 64 + lane;
         };
-#if RTC_GEO_CLASSES
-        /* sub-list 4 c + tile % 4 for the class c of the tile's candidate count, the tiles with the longest lists (the
-         * dearest pixels: every sample tests them) first in the concatenated item order */
-        const int cls = nCand >= 32 ? 0 : nCand >= 16 ? 1 : nCand >= 8 ? 2 : 3;
-        append(b, cls * 4 + (tile & 3));
-#elif RTC_GEO_HINT
-        /* the pixels the hint marks go to sub-lists 0-3 (the head of the item order), the tile's others to sub-lists 4-15
-         * spread by tile; sub-list l receives only pixels of tiles with tile % 4 == l % 4 (geoCap: a quarter of the
-         * tiles' pixels) */
-        const bool marked = P.tileHint && ((b >> lane) & 1ull) && P.tileHint[(size_t)tile * 64 + lane] != 0;
-        const unsigned long long hb = __ballot(marked);
-        if (marked)
-            P.tileHint[(size_t)tile * 64 + lane] = 0; /* this launch's geometry kernel marks it again */
-        if (hb)
-            append(hb, tile & 3);
-        if (b & ~hb)
-            append(b & ~hb, 4 * (1 + (tile >> 2) % 3) + (tile & 3));
-#else
         append(b, tile % kGeoLists);
-#endif
     }
     if (lane == 0 && b)
         atomicAdd(&wgWeight, (unsigned)__popcll(b));
@@ -1854,11 +1075,8 @@ __global__ __launch_bounds__(kSegSlots) void rtc_reduce_segments(unsigned long l
 }
 
 
-#ifndef RTC_MIN_WAVES
-#define RTC_MIN_WAVES 1
-#endif
 template <bool SPHERES, bool DEBUG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_WAVES))) void rtc_render_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1))) void rtc_render_kernel(
     RenderParams P)
 {
 #ifdef RTC_DIAG
@@ -1878,7 +1096,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     /* general-path records in LDS (small scenes) and the powf tables */
     __shared__ DevTri sTris[kLdsTris];
     __shared__ PowTablesLds sPow;
-    const bool useLds = RTC_GEN_LDS && P.triPadded <= kLdsTris;
+    const bool useLds = P.triPadded <= kLdsTris;
     if (useLds) {
         for (int i = threadIdx.x; i < P.triPadded; i += kBlock)
             sTris[i] = P.tris[i];
@@ -2057,48 +1275,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTC_MIN_
     flush_counters(P, segCalls, segTraced, segTests, lane);
 }
 
-#ifndef RTC_SKY_UNROLL
-#define RTC_SKY_UNROLL 2
-#endif
-
-/* True when the bounce ray (pos, dir) provably cannot hit any triangle of cluster K (see DevCluster): the
- * half-line's distance to the ball centre exceeds T >= r + eps.  rho = |dir|_1 >= |dir| bounds the eps terms;
- * dd = dir.dir.  With w = centre - pos and b = w.dir, the half-line's closest point to the centre is interior
- * when b > 0, at distance |w x dir| / |dir|, else the origin, at |w|.  |w x dir|^2 is evaluated by Lagrange's
- * identity w2 dd - b^2 (FMA dots, each within 3u relative; the cancellation is covered by an explicit margin of
- * 25u w2 dd >= the evaluation error) and compared with T^2 dd: the 1.00001 factor on T covers dd's own error.
- * The f32 evaluation of w, S and T is covered by the gamma terms (rtc_build_clusters).  NaN never culls.
- * cluster_terms: the per-(origin, cluster) values, culled_by: the per-direction test (the chain kernel tabulates
- * the first for a pixel's primary hit point, where every first bounce starts). */
-struct ClusterTerms {
-    V3 w;
-    float w2, A, B; /* T = (A + rho B) * 1.00001 */
-};
-__device__ __forceinline__ ClusterTerms cluster_terms(V3 pos, const DevCluster &K)
-{
-    ClusterTerms t;
-    t.w = sub(V3{K.cx, K.cy, K.cz}, pos);
-    const float S = fabsf(t.w.x) + fabsf(t.w.y) + fabsf(t.w.z) + K.r; /* >= |pos - A| for every vertex A */
-    t.w2 = fmaf(t.w.z, t.w.z, fmaf(t.w.y, t.w.y, t.w.x * t.w.x));
-    t.A = (K.r + kClusterGamma * S) + K.gammaE;
-    t.B = fmaf(K.beta, S, K.alpha);
-    return t;
-}
-__device__ __forceinline__ bool culled_by(const ClusterTerms &t, V3 dir, float rho, float dd)
-{
-    const float T = fmaf(rho, t.B, t.A) * 1.00001f;
-    const float T2 = T * T;
-    const float b = fmaf(t.w.z, dir.z, fmaf(t.w.y, dir.y, t.w.x * dir.x));
-    const float wd = t.w2 * dd;
-    const float x2 = fmaf(-b, b, wd);
-    return b > 0.f ? (x2 - 1.5e-6f * wd > T2 * dd) : (t.w2 > T2);
-}
-__device__ __forceinline__ float dir_dd(V3 dir) { return fmaf(dir.z, dir.z, fmaf(dir.y, dir.y, dir.x * dir.x)); }
-__device__ __forceinline__ bool cluster_culled(V3 pos, V3 dir, float rho, float dd, const DevCluster &K)
-{
-    return culled_by(cluster_terms(pos, K), dir, rho, dd);
-}
-
 /* LDS writes of this wave visible to its other lanes (the wave is the only user of the region) */
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -2107,120 +1283,22 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* Sky tiles of the split launch (rtc_render_sky): one wave per 8x8 tile (one-wave workgroups, or four per 16x16 block); the waves of
- * tiles whose pixels all have primary candidates return at once (rtc_render_chain renders those).  Few registers, so many
- * waves per SIMD hide the latency of the environment's double-precision chains. */
+/* The sky pass (rtc_render_sky_rows): every pixel whose primary ray provably misses, few registers, so many waves per SIMD
+ * hide the latency of the environment's double-precision chains.  <= 64 VGPRs: two sky waves fit where one chain wave
+ * retires (frame -1.5 %, round 4). */
 #ifndef RTC_SKY_WAVES
-#define RTC_SKY_WAVES 8 /* <= 64 VGPRs: two sky workgroups fit where one chain workgroup retires (frame -1.5 %, round 4) */
+#define RTC_SKY_WAVES 8
 #endif
-/* kSkyWaves waves per workgroup: 4 (a 16x16 block) or 1 (one 8x8 tile).  One-wave workgroups fit the registers and wave
- * slots the co-resident chain workgroups leave free at a finer grain (round 4: whole 1080p frame -1 %, 4K -0.6 %, the
- * 1080p 1/8 share -2 %), but the 1/4 share (518 k px) took 3.5 % longer with them, so small shares of more than 400 k
- * pixels keep 4 (profiles/r04_zd_ab_sky_wg.log) */
-template <int kSkyWaves>
-__global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky(
-    RenderParams P, const unsigned *__restrict__ tileW)
-{
-    static_assert(kSkyWaves == 4 || kSkyWaves == 1, "a sky workgroup is a 16x16 block or one 8x8 tile");
-    __shared__ PowTablesLds sPow;
-    __shared__ __attribute__((aligned(4))) unsigned char sSkyRow[kSkyWaves][8][24];
-    sPow.fill(threadIdx.x);
-    __syncthreads();
-    sPow.attach(P.env);
-    const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;
-    unsigned segCalls = 0, segTraced = 0;
-    {
-        /* the 16x16 block (bx, by) and this wave's 8x8 tile w16 in it (one-wave workgroups: grid twice as wide and tall) */
-        const int bx = kSkyWaves == 4 ? (int)blockIdx.x : (int)blockIdx.x >> 1;
-        const int by = kSkyWaves == 4 ? (int)blockIdx.y : (int)blockIdx.y >> 1;
-        const int w16 = kSkyWaves == 4 ? __builtin_amdgcn_readfirstlane(lw) : (int)((blockIdx.y & 1) * 2 + (blockIdx.x & 1));
-        /* pixels without a primary candidate: their primary ray misses every triangle (the filter is exact-safe),
-         * so every sample is one segment ending in the sky, in tiles with geometry pixels too (rtc_render_chain takes only the geometry pixels) */
-        const int t = (by * 2 + (w16 >> 1)) * (P.blocksX * 2) + bx * 2 + (w16 & 1);
-        const unsigned long long geo = tileW[t] > 0 ? P.pixMask[t] : 0ull;
-        if (geo == ~0ull)
-            return;
-        PixelRay px;
-        px.x = bx * kTileW + (w16 & 1) * 8 + (lane & 7);
-        px.r = by * kTileH + (w16 >> 1) * 8 + (lane >> 3);
-        px.valid = px.x < P.width && px.r < P.rows;
-        px.y = launch_row_y(P, px.r);
-        px.dir = primary_dir(P, px.x, px.y);
-        px.valid = px.valid && !((geo >> lane) & 1ull);
-        V3 acc{0.f, 0.f, 0.f};
-        if (px.valid && P.spp > 0 && P.maxBounce > 0) {
-            /* see the skyTile path of rtc_render_kernel.  Hoisted mode evaluates the primary ray's miss once
-             * (a function of the pixel, like its closest hit); faithful mode evaluates it every sample. */
-            if (P.hoist) {
-                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
-                for (int s = 0; s < P.spp; ++s)
-                    acc = add(acc, mul(l, P.invSpp));
-            } else {
-#pragma unroll RTC_SKY_UNROLL
-                for (int s = 0; s < P.spp; ++s) {
-#if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the sky pass's environment cost) */
-                    const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(px.dir.y + (float)s * 1e-9f, 0.f));
-#else
-                    const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(px.dir, P.env), V3{1.f, 1.f, 1.f}));
-#endif
-                    acc = add(acc, mul(l, P.invSpp));
-                }
-            }
-            segCalls = (unsigned)P.spp;
-            segTraced = P.hoist ? 1u : (unsigned)P.spp;
-        }
-        /* Color[] (vec3ToColor, main.c:101): a tile row whose 8 pixels are all this kernel's goes out as six
-         * dword stores of its 24 bytes (staged in LDS) instead of 24 byte stores; rows shared with geometry
-         * pixels (written by the other kernel) or cut by the frame edge keep byte stores */
-        const unsigned char c0 = float_to_u8(acc.x), c1 = float_to_u8(acc.y), c2 = float_to_u8(acc.z);
-        const unsigned long long full = __ballot(px.valid);
-        const int row = lane >> 3;
-        const bool aligned = (P.width & 3) == 0 && ((size_t)P.colors & 3) == 0;
-        const bool packed = aligned && ((full >> (row * 8)) & 0xffull) == 0xffull;
-        unsigned char *rowBytes = sSkyRow[lw][row];
-        if (packed) {
-            rowBytes[3 * (lane & 7)] = c0;
-            rowBytes[3 * (lane & 7) + 1] = c1;
-            rowBytes[3 * (lane & 7) + 2] = c2;
-        }
-        wave_lds_sync();
-        if (lane < 48) {
-            const int rr = lane / 6, dw = lane - rr * 6;
-            if (aligned && ((full >> (rr * 8)) & 0xffull) == 0xffull) {
-                /* this row's first pixel: column 0 of the tile, row rr */
-                const int x0 = bx * kTileW + (w16 & 1) * 8;
-                const int r0 = by * kTileH + (w16 >> 1) * 8 + rr;
-                unsigned *dst = (unsigned *)(P.colors + 3 * ((size_t)r0 * (size_t)P.width + (size_t)x0));
-                dst[dw] = ((const unsigned *)sSkyRow[lw][rr])[dw];
-            }
-        }
-        if (px.valid) {
-            const size_t o = (size_t)px.r * (size_t)P.width + (size_t)px.x;
-            if (!packed) {
-                P.colors[3 * o] = c0;
-                P.colors[3 * o + 1] = c1;
-                P.colors[3 * o + 2] = c2;
-            }
-            if (P.accum) {
-                P.accum[3 * o] = acc.x;
-                P.accum[3 * o + 1] = acc.y;
-                P.accum[3 * o + 2] = acc.z;
-            }
-        }
-    }
-    flush_counters(P, segCalls, segTraced, 0ull, lane);
-}
-
-/* Sky pixels by row strips (round 5, RTC_SKY_ROWS): each wave takes 64 consecutive pixels of one launch row (workgroups of
+/* Sky pixels by row strips (round 5): each wave takes 64 consecutive pixels of one launch row (workgroups of
  * kSkyWaves waves: kSkyWaves consecutive rows), so a strip of Color is 192 B = three whole 64-B lines when the row starts
  * on a line (every BASELINE width: 1920 * 3 and 3840 * 3 are multiples of 64), written by twelve 16-B stores staged in
  * LDS.  The 8x8-tile waves wrote 24-B tile rows that straddle lines shared with the neighbouring tiles' waves, so every
  * line was written back partially two or three times (sky WRITE_SIZE 12.0 MB per 1080p launch for 6.0 MB of Color,
  * VERDICT r04 #5).  A strip holding geometry pixels (rtc_render_chain writes those, maybe concurrently) or cut by the frame
- * edge writes its sky pixels' bytes only.  Same pixels, same per-sample environment loop, same values. */
-#ifndef RTC_SKY_ROWS
-#define RTC_SKY_ROWS 1
-#endif
+ * edge writes its sky pixels' bytes only.  Same pixels, same per-sample environment loop, same values.  kSkyWaves waves per
+ * workgroup: 1, or 4 for small shares of more than 400 k pixels (one-wave workgroups fill the registers and wave slots
+ * the co-resident chain workgroups leave free at a finer grain -- whole frames -1 %, the 1080p 1/8 share -2 % -- but
+ * the 1/4 share took 3.5 % longer with them, profiles/r04_zd_ab_sky_wg.log). */
 template <int kSkyWaves>
 __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky_rows(
     RenderParams P, const unsigned *__restrict__ tileW)
@@ -2249,23 +1327,20 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
     const V3 dir = primary_dir(P, x, y);
     V3 acc{0.f, 0.f, 0.f};
     if (valid && P.spp > 0 && P.maxBounce > 0) {
-        /* see rtc_render_sky: hoisted mode evaluates the primary ray's miss once, faithful mode every sample */
+        /* hoisted mode evaluates the primary ray's miss once (a function of the pixel, like its closest hit), faithful
+         * mode every sample */
         if (P.hoist) {
             const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f}));
             for (int s = 0; s < P.spp; ++s)
                 acc = add(acc, mul(l, P.invSpp));
         } else {
-#pragma unroll RTC_SKY_UNROLL
+#pragma unroll 2
             for (int s = 0; s < P.spp; ++s) {
 #if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the environment's cost) */
                 const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y + (float)s * 1e-9f, 0.f));
 #else
                 /* raytracing.c:291 with rayColor (1, 1, 1): 0 + environment (environment_miss_term: acc starts at +0) */
-#ifndef RTC_SKY_MISS_FULL
                 const V3 l = environment_miss_term(dir, P.env);
-#else /* the reference's adds as written (same values; round 5 A/B) */
-                const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f}));
-#endif
 #endif
                 acc = add(acc, mul(l, P.invSpp)); /* main.c:99 */
             }
@@ -2315,22 +1390,16 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
  * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
  * Work: one wave per geometry pixel, from the tile cull's sub-lists (see the kernel). */
-#ifndef RTC_SHARE_CHAIN_CS
-#define RTC_SHARE_CHAIN_CS 1
-#endif
 constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
 /* Shares (row stride > 1) of up to this many pixels are "small": they sum in-kernel, run 4 chain workgroups per CU and,
- * pipelined, prepare, cull and run their geometry kernel on the two cull streams (RTC_SHARE_CHAIN_CS).  Round 4 raised it
+ * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
 #ifndef RTC_INLINE_SUM_PIXELS
 #define RTC_INLINE_SUM_PIXELS 600000
 #endif
 constexpr size_t kInlineSumPixels = RTC_INLINE_SUM_PIXELS;
-#ifndef RTC_CHAIN_BLOCK
-#define RTC_CHAIN_BLOCK 256
-#endif
-constexpr int kChainBlock = RTC_CHAIN_BLOCK; /* threads per chain workgroup */
+constexpr int kChainBlock = 256; /* threads per chain workgroup (two-wave workgroups were slower everywhere, r04_ze) */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
  * in the chain kernel's idle issue slots instead of waiting for its tail, and the launch stream's small kernels are no
@@ -2341,9 +1410,6 @@ constexpr int kChainBlock = RTC_CHAIN_BLOCK; /* threads per chain workgroup */
  * exactly the resident capacity, no second round.  (RTC_CHAIN_WGS_FULL / _HIT are defined with kSkySlots.) */
 #ifndef RTC_CHAIN_WGS_SHARE
 #define RTC_CHAIN_WGS_SHARE 3 /* 1/4 share 0.116 -> 0.113 ms, 1/8 share 0.075 -> 0.074 ms (round 4, r04_za) */
-#endif
-#ifndef RTC_CHAIN_UNROLL
-#define RTC_CHAIN_UNROLL 4 /* the pair passes' record loop (round 5: 4 vs 2, fsuzane -1 %, headline within noise; same registers) */
 #endif
 #ifndef RTC_CHAIN_WAVES
 #define RTC_CHAIN_WAVES 4
@@ -2368,41 +1434,28 @@ typedef float f2 __attribute__((ext_vector_type(2)));
  * state advanced by 7 i draws).  The values are the same function of the same state, so the frame is unchanged;
  * what goes is most of the divergent Box-Muller passes of the bounce iterations with a hit (scenes whose rays hit
  * several times: fsuzane 2.00 -> 1.93 ms per frame, 1.77 with the dense culls below). */
-#ifndef RTC_DRAW_TABLE
-#define RTC_DRAW_TABLE 1
-#endif
-#ifndef RTC_CHAIN_PAIRS
-#define RTC_CHAIN_PAIRS 1024
-#endif
+constexpr int kChainPairs = 1024;
 struct ChainWaveLds {
     float4 cl[kChunkClusters][2]; /* first bounces: the clusters' origin terms (ClusterTerms) */
     unsigned long long key[64];   /* closest hit per lane, (dst bits << 32) | index */
     /* lane | cluster << 6 (or lane | record << 6), cluster-major; a full list is run through the passes and
      * refilled.  Its size keeps a block (4 waves + the staged records of one chunk) within 40 KB of LDS: four
      * blocks per CU, the 4 waves per SIMD that 128 VGPRs allow */
-    unsigned short pair[RTC_CHAIN_PAIRS];
-#if RTC_DRAW_TABLE
+    unsigned short pair[kChainPairs];
     float4 draw[64]; /* the window's hit draws by state index jn + i: RandomDirection's vector, the roulette value */
-#endif
 };
 constexpr unsigned long long kNoHitKey = ((unsigned long long)0x497423F0u << 32) | 0xFFFFFFFFull; /* 999999.f */
 static_assert(kChunkClusters <= 32, "cluster masks are 32-bit");
-static_assert(RTC_CHAIN_PAIRS >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
-static_assert(RTC_CHAIN_PAIRS * sizeof(unsigned short) >= 3 * 64 * sizeof(float), "a window's staged samples fit the list");
+static_assert(kChainPairs >= 64 * kClusterSize, "one cluster's pairs of a full wave fit the list");
+static_assert(kChainPairs * sizeof(unsigned short) >= 3 * 64 * sizeof(float), "a window's staged samples fit the list");
 /* rtc_render_chain's static LDS (powf tables, the waves' ChainWaveLds, the work counter) and the block budget
  * that keeps 4 blocks (16 waves) per CU */
-#ifndef RTC_BM_LDS
-#define RTC_BM_LDS 0 /* 1: the Box-Muller tables in LDS (BmTablesLds; round 5: frame and shares unchanged, chain -1 %) */
-#endif
-constexpr size_t kChainStaticLds = sizeof(PowTablesLds) + (RTC_BM_LDS ? sizeof(BmTablesLds) : 0) +
+constexpr size_t kChainStaticLds = sizeof(PowTablesLds) +
                                    (kChainBlock / 64) * sizeof(ChainWaveLds) + 64 +
-                                   kChunkClusters * sizeof(DevCluster) /* sCl (RTC_DENSE_CULL) */;
+                                   kChunkClusters * sizeof(DevCluster) /* sCl (the dense culls) */;
 constexpr size_t kCuLds = 160 * 1024; /* gfx950 LDS per CU */
 /* the block LDS that keeps the chain workgroups per CU at most n: above kCuLds / (n + 1) */
 constexpr size_t chain_lds_floor(int n) { return n >= 4 ? 0 : kCuLds / (size_t)(n + 1) + 256; }
-#ifndef RTC_INLINE_ALL
-#define RTC_INLINE_ALL 0 /* every launch sums in-kernel */
-#endif
 
 /* The pair passes: entry i of W.pair (i < n) is a (lane, cluster) pair -- the cluster's 8 records; the owner's ray
  * by ds_bpermute from the owner lane (every lane takes part), the exact-safe filter, the reference arithmetic for
@@ -2443,7 +1496,7 @@ __device__ __forceinline__ void chain_pair_passes(const RenderParams &P, int n, 
             const int r0 = (c0 + (int)(pr >> 6)) * kClusterSize, nRec = P.clusterCount * kClusterSize;
             auto rec = [&](int j) -> DevTri { return MULTI ? P.clTris[r0 + j] : rec_soa(sRec, nRec, r0 + j); };
             unsigned surv = 0;
-#pragma unroll RTC_CHAIN_UNROLL
+#pragma unroll 4 /* (round 5: 4 vs 2, fsuzane -1 %, headline within noise; same registers) */
             for (int j = 0; j < kClusterSize; ++j)
                 surv |= (unsigned)general_filter(rpos, rdir, rec(j)) << j;
             while (surv) {
@@ -2487,15 +1540,10 @@ __device__ __forceinline__ void chain_pair_passes_cl(int n, const float4 *__rest
 /* Dense cluster culls (single-chunk scenes, bounce segments after the first): with a live lanes and nCl clusters, the
  * per-lane loop issues nCl culls for the wave however few lanes are live; instead the wave takes the a * nCl (live
  * lane, cluster) culls 64 at a time -- cluster-major, so the pairs kept come out in the per-lane loop's order -- the
- * owner's ray by ds_bpermute, the cluster from LDS.  Taken while a <= RTC_DENSE_CULL_MAX (fsuzane 1.93 -> 1.77 ms per
+ * owner's ray by ds_bpermute, the cluster from LDS.  Taken while a <= kDenseCullMax (fsuzane 1.93 -> 1.77 ms per
  * frame with 16, 1.80 with 32; the headline frame, whose later bounces are rare, within noise). */
-#ifndef RTC_DENSE_CULL
-#define RTC_DENSE_CULL 1
-#endif
-#ifndef RTC_DENSE_CULL_MAX
-#define RTC_DENSE_CULL_MAX 16
-#endif
-static_assert(RTC_DENSE_CULL_MAX * kChunkClusters <= RTC_CHAIN_PAIRS, "a dense cull's pairs fit the list");
+constexpr int kDenseCullMax = 16;
+static_assert(kDenseCullMax * kChunkClusters <= kChainPairs, "a dense cull's pairs fit the list");
 static_assert(sizeof(ChainWaveLds::cl) >= 64 * sizeof(int), "the dense cull's owner lanes fit W.cl");
 
 template <bool MULTI, bool COUNT>
@@ -2550,7 +1598,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(live >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)live, 0u));
             /* (the workgroup's LDS copy of the clusters: a global load here was a round trip on every window) */
-            const ClusterTerms t = cluster_terms(p0, RTC_DENSE_CULL ? sCl[lane] : P.clusters[lane]);
+            const ClusterTerms t = cluster_terms(p0, sCl[lane]);
             W.cl[pos][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
             W.cl[pos][1] = make_float4(t.A, t.B, __int_as_float(lane), __int_as_float((int)r8l));
         }
@@ -2572,10 +1620,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         unsigned cm = 0;
         int n = 0;
         DSECT_BEGIN(dc3);
-#if RTC_DENSE_CULL
         const unsigned long long inM = __ballot(in);
         const int nIn = (int)__popcll(inM);
-        const bool dense = !MULTI && !table && nIn <= RTC_DENSE_CULL_MAX;
+        const bool dense = !MULTI && !table && nIn <= kDenseCullMax;
         if (dense) {
             int *own = (int *)&W.cl[0][0]; /* W.cl is free outside the first bounce's table mode */
             int *kept = own + 64;          /* COUNT: per owner lane, clusters kept (+ 1 << 16 for the scene's last) */
@@ -2614,9 +1661,6 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                         (unsigned)(kc >> 16) * (unsigned)(P.clusterCount * kClusterSize - P.triCount);
             }
         }
-#else
-        constexpr bool dense = false;
-#endif
         /* table mode: bit j of cm = the j-th live cluster kept (branch-free body over the compacted terms) */
         const int nLive = __popcll(live);
         if (dense) {
@@ -2639,7 +1683,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         }
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
-        constexpr int kCap = RTC_CHAIN_PAIRS;
+        constexpr int kCap = kChainPairs;
         if (dense) {
         } else if (table) {
             /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
@@ -2735,7 +1779,7 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 /* Primary segments over the tile's candidates (rtc_render_chain) with the filter records staged in LDS (null: from
  * global memory): the filter's record is an LDS read instead of a dependent scalar load per candidate; DevPrimX
  * (survivors only) stays global.  Same operations as closest_primary_listed. */
-__device__ __forceinline__ void closest_primary_listed_lds(V3 dir, Closest &c, const unsigned long long *__restrict__ mask,
+__device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P, V3 dir, Closest &c, const unsigned long long *__restrict__ mask,
                                                            unsigned long long m0, unsigned long long m1,
                                                            const DevPrimF *__restrict__ sF, bool staged)
 {
@@ -2802,9 +1846,8 @@ template <bool MULTI, bool COUNT> /* MULTI: more than one chunk of clusters (chu
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
-#if RTC_CHAIN_PRIO > 0
-    __builtin_amdgcn_s_setprio(RTC_CHAIN_PRIO);
-#endif
+    if (RTC_CHAIN_PRIO > 0)
+        __builtin_amdgcn_s_setprio(RTC_CHAIN_PRIO);
     DSECT_BEGIN(dtot);
     DMARK_INIT(dcur);
 #ifdef RTC_DIAG
@@ -2814,23 +1857,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     extern __shared__ __attribute__((aligned(64))) unsigned char sDyn[];
     __shared__ PowTablesLds sPow;
-#if RTC_BM_LDS
-    __shared__ BmTablesLds sBm;
-    static_assert(kChainBlock >= 192, "BmTablesLds::fill takes 192 threads");
-    sBm.fill(threadIdx.x);
-#define RTC_CHAIN_BM_TABS , sBm.log, sBm.cos
-#else
-#define RTC_CHAIN_BM_TABS
-#endif
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
-#if RTC_DENSE_CULL
     __shared__ DevCluster sCl[kChunkClusters]; /* single-chunk scenes: the clusters, for the dense culls */
     if (!MULTI && threadIdx.x < P.clusterCount && threadIdx.x < kChunkClusters)
         sCl[threadIdx.x] = P.clusters[threadIdx.x];
-#else
-    const DevCluster *sCl = nullptr;
-#endif
     if (threadIdx.x == 0)
         sWork = 0;
     sPow.fill(threadIdx.x);
@@ -2856,20 +1887,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * shortened the kernel 4 % but made every workgroup retire at its end, so the sky pass no longer filled the
      * tail: frame 0.396 -> 0.42 ms). */
     int nextIt = 0;
-#if RTC_ITEM_COUNTERS > 0
-    /* Experiment (round 5, not kept): global counters.  With a fixed 1/grid of the items per workgroup the
-     * workgroups' totals differ (item costs vary ~5x): at 1080p the kernel's span is ~20 % past its waves' mean busy
-     * time (per-item timings, tools/item_spread.py).  Here workgroup b takes items c + k * kItemCounters, c = b %
-     * kItemCounters (XCD b % 8 with 8), k from counter c, one returning atomic per item issued one item ahead.  The
-     * kernel got 6 % shorter but the frame 3-4 % longer (the sky pass no longer fills its tail) and the small shares
-     * 17-28 % longer (the counters saturate: ~30 atomics per us on one address); profiles/r05_xc_ab_item_counters.log */
-    int *const itemCounter = P.geoCount + ((int)blockIdx.x % kItemCounters) * kGeoCountStride + kItemCounterOffset;
-#define RTC_NEXT_ITEM() ((int)blockIdx.x % kItemCounters + atomicAdd(itemCounter, 1) * kItemCounters)
-#else
-#define RTC_NEXT_ITEM() ((int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x)
-#endif
+    /* (global item counters instead, round 5: the kernel 6 % shorter, the frame 3-4 % longer -- the sky pass no longer
+     * fills its tail -- and small shares 17-28 % longer, profiles/r05_xc_ab_item_counters.log) */
+    const auto next_item = [&]() { return (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x; };
     if (lane == 0)
-        nextIt = RTC_NEXT_ITEM();
+        nextIt = next_item();
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
      * segment where they are used: KARG) */
 #ifdef RTC_DIAG_COUNT /* diagnostic variant: the test counters on in every launch (rtc_diag_itemlog's tests) */
@@ -2900,9 +1922,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * order and are waited for by vmcnt, so a scalar wait never completes them early.  Each lives in one register that
      * is consumed before it is reloaded (a loop-carried copy of an in-flight load would wait for it at the copy), and
      * neither is in flight at a loop preheader that flushes vmcnt (after the bounce loop, the walk's did). */
-#ifndef RTC_ITEM_PREFETCH
-#define RTC_ITEM_PREFETCH 1
-#endif
     const auto entry_of = [&](int it2) -> size_t {
         const int l = (int)__popcll(__ballot(lane < kGeoLists && incl <= it2));
         const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
@@ -2914,12 +1933,12 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     };
     int it = __builtin_amdgcn_readfirstlane(nextIt);
     unsigned vc = 0, vm = 0; /* the current item's entry and mask dwords (vector registers) */
-    if (RTC_ITEM_PREFETCH && it < nItems) {
+    if (it < nItems) {
         vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
         vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
     }
     if (lane == 0)
-        nextIt = RTC_NEXT_ITEM();
+        nextIt = next_item();
     DMARK(dcur, 19); /* prologue: staging, tables, the first item */
     for (;;) {
         if (it >= nItems)
@@ -2933,26 +1952,20 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const unsigned long long dSect = lane < kItemSects ? s_rtc_sect[threadIdx.x >> 6][item_sect_id(lane)] : 0ull;
         unsigned long long dItemTests = 0;
 #endif
-#if RTC_ITEM_PREFETCH
         const int code = __builtin_amdgcn_readfirstlane((int)vc);
         const unsigned long long m0 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 0) |
                                       (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 1) << 32;
         const unsigned long long m1 = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 2) |
                                       (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)vm, 3) << 32;
-#else /* round 4: scalar loads at the item's start */
-        const int code = __builtin_amdgcn_readfirstlane(KCONST(KARG(geoList))[entry_of(it)]);
-        const unsigned long long *mk = KARG(tileMask) + (size_t)(code >> 6) * P.maskWords;
-        const unsigned long long m0 = KCONST(mk)[0], m1 = P.maskWords > 1 ? KCONST(mk)[1] : 0ull;
-#endif
         /* the next item: its number (the LDS counter read at this item's previous start), its entry, and the counter for
          * the one after */
         const int itNext = __builtin_amdgcn_readfirstlane(nextIt);
-        if (RTC_ITEM_PREFETCH && itNext < nItems)
+        if (itNext < nItems)
             vc = gload(KARG(geoList), entry_of(itNext) + (size_t)vzero());
         /* the next item's mask dwords requested (none needed past the end) */
-        bool maskNext = !RTC_ITEM_PREFETCH || itNext >= nItems;
+        bool maskNext = itNext >= nItems;
         if (lane == 0)
-            nextIt = RTC_NEXT_ITEM();
+            nextIt = next_item();
         const int tile = code >> 6, bit = code & 63;
         const int tilesX = KARG(blocksX) * 2;
         const int x = (tile % tilesX) * 8 + (bit & 7), r = (tile / tilesX) * 8 + (bit >> 3);
@@ -2974,7 +1987,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const bool deferred = it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
-            closest_primary_listed_lds(pdir, prim, mask, m0, m1, sPF, pfStaged);
+            closest_primary_listed_lds(P, pdir, prim, mask, m0, m1, sPF, pfStaged);
             if (counting && lane == 0) {
                 segTraced++;
                 segTests += L;
@@ -2985,9 +1998,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         float acc = 0.f;
         int k = 0;       /* samples accumulated */
         unsigned jn = 0; /* state index (in units of 7 draws) of sample k */
-        int nWin = 0;    /* windows of this item (RTC_GEO_HINT) */
         while (k < P.spp && P.maxBounce > 0) {
-            ++nWin;
             /* window: the state indices the remaining samples likely span (the pixel's hits per sample so far, a
              * margin; the first window assumes one hit per sample) */
             const int need = P.spp - k;
@@ -3020,7 +2031,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         if (P.hoist) {
                             c = prim;
                         } else {
-                            closest_primary_listed_lds(dir, c, mask, m0, m1, sPF, pfStaged);
+                            closest_primary_listed_lds(P, dir, c, mask, m0, m1, sPF, pfStaged);
                             if (counting)
                                 tests += L;
                         }
@@ -3040,12 +2051,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                     DMARK(dcur, bounce1 ? 17 : 20); /* bounce trace: the first bounce (17), later ones (20); 14 table, 3
                                                      * cull, 4 pair build, 5 pair passes inside */
                 }
-#if RTC_DRAW_TABLE
-                /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the table */
+                /* the state advance of this iteration's hits (7 draws per earlier hit), for lanes past the draw table */
                 RngJump J{1u, 0u};
                 if (!first && __ballot(alive && c.idx >= 0 && lane + iter >= nAct))
                     J = rng_jump_by(7u * (unsigned)iter); /* wave-uniform */
-#endif
                 if (alive) {
                     if (counting)
                         calls++;
@@ -3057,8 +2066,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         const V3 hitPoint = add(pos, mul(dir, c.dst)); /* raytracing.c:238 */
                         DevTri T;
                         DevMat M;
-                        DSECT_BEGIN(dh8);
-                        if (RTC_SMEM && first) { /* the pixel's primary hit: the same triangle in every lane */
+                        if (first) { /* the pixel's primary hit: the same triangle in every lane */
                             const int u = __builtin_amdgcn_readfirstlane(c.idx);
                             T = KLOAD(KARG(tris), u);
                             M = KLOAD(KARG(mats), u);
@@ -3066,33 +2074,21 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                             T = P.tris[c.idx]; /* (kernel-argument pointers: global loads, not flat) */
                             M = P.mats[c.idx];
                         }
-#ifdef RTC_DIAG_HITSPLIT /* diagnostic: the hit's loads (and any older ones still in flight) apart from its draws */
-                        __builtin_amdgcn_s_waitcnt(0);
-                        DSECT_END(dh8, 8);
-#endif
-                        DSECT_BEGIN(dh9);
                         const V3 normal{T.nx, T.ny, T.nz}, color{M.r, M.g, M.b};
-#if RTC_DRAW_TABLE
-                        /* the hit draws (see RTC_DRAW_TABLE): the primary hit computes the lane's own and enters
+                        /* the hit draws (see ChainWaveLds::draw): the primary hit computes the lane's own and enters
                          * them in the table (every active lane hits there: one primary ray per wave); a later hit
                          * reads entry lane + iter, or computes it when that is past the window's active lanes */
                         float4 D;
                         if (first || lane + iter >= nAct) {
                             unsigned s = first ? rng : rng * J.a + J.c;
-                            const V3 rd = random_direction(s RTC_CHAIN_BM_TABS);
+                            const V3 rd = random_direction(s);
                             D = make_float4(rd.x, rd.y, rd.z, random_value(s));
                             if (first)
                                 W.draw[lane] = D; /* read in later iterations, after chain_trace_pairs' LDS syncs */
                         } else {
                             D = W.draw[lane + iter];
                         }
-#ifdef RTC_DIAG_HITSPLIT
-                        DSECT_END(dh9, 9);
-#endif
                         const V3 diffuseDir = normalized(add(normal, V3{D.x, D.y, D.z}));
-#else
-                        const V3 diffuseDir = normalized(add(normal, random_direction(rng RTC_CHAIN_BM_TABS)));
-#endif
                         const V3 specularDir = reflect(dir, normal);
                         dir = lerp(diffuseDir, specularDir, M.smoothness);
                         pos = hitPoint;
@@ -3100,11 +2096,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         light = add(light, mulv(emitted, rayColor));
                         rayColor = mulv(rayColor, color);
                         const float p = fmax_ref(fmax_ref(rayColor.x, rayColor.y), rayColor.z);
-#if RTC_DRAW_TABLE
                         endSample = p < D.w;
-#else
-                        endSample = p < random_value(rng);
-#endif
                         if (!endSample) {
                             rayColor = mul(rayColor, rcp_cr(p)); /* (float)(1.0 / p) */
                             bounce++;
@@ -3113,13 +2105,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         DSECT_END(dc2, 2);
                     } else {
                         DSECT_BEGIN(dc6);
-#ifdef RTC_AB_CHEAP_ENV_CHAIN /* timing experiment only (the environment's cost in the chain kernel) */
-                        light = add(light, mulv(lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y, 0.f)), rayColor));
-#else
                         EnvParams env = KARG(env); /* the launch's sky and sun, the powf tables in LDS */
                         sPow.attach(env);
                         light = add(light, mulv(environment(dir, env), rayColor)); /* raytracing.c:291 */
-#endif
                         endSample = true;
                         DSECT_END(dc6, 6);
                     }
@@ -3243,8 +2231,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         }
         if (!maskNext) /* (an item without a bounce iteration) */
             vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
-        if (RTC_GEO_HINT && nWin > 1 && lane == 0 && KARG(tileHint)) /* the next launch's tile cull orders it first */
-            KARG(tileHint)[code] = 1;
 #ifdef RTC_DIAG
         if (lane == 0 && it < kItemLog) {
             g_rtc_itemlog[it][0] = dItemT0;
@@ -3296,22 +2282,16 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 
 /* A kernel launch whose completion also records `stop` (null: a plain launch): the event is the dispatch's own
  * completion signal, so the stream gets no separate marker packet -- each marker on the launch stream cost ~5-7 us
- * before the next kernel (RTC_EXT_EVENTS 0: hipEventRecord after the launch) */
-#ifndef RTC_EXT_EVENTS
-#define RTC_EXT_EVENTS 1
-#endif
+ * before the next kernel (round 3: a hipEventRecord after the launch) */
 template <typename... K, typename... A>
 static hipError_t launch_stop(void (*k)(K...), dim3 g, dim3 b, size_t sh, hipStream_t st, hipEvent_t stop, A... args)
 {
-    if (stop && RTC_EXT_EVENTS) {
+    if (stop) {
         hipExtLaunchKernelGGL(k, g, b, (std::uint32_t)sh, st, nullptr, stop, 0u, args...);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k, g, b, sh, st, args...);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && stop)
-        e = hipEventRecord(stop, st);
-    return e;
+    return hipGetLastError();
 }
 
 static SkyKey sky_key(const RenderParams &P)
@@ -3346,21 +2326,11 @@ static EnvParams env_of(const Scene &s)
     return e;
 }
 
-__host__ __device__ static inline V3 v3(vec3 v) { return V3{v.x, v.y, v.z}; }
 
-#ifndef RTC_SIDE_STREAM
-#define RTC_SIDE_STREAM 1
-#endif
-#ifndef RTC_CULL_STREAM
-#define RTC_CULL_STREAM 1
-#endif
 #ifdef RTC_AB_NO_SLOTS
-#define RTC_AB_NO_SLOTS_ON 1
+constexpr bool kAbNoSlots = true; /* timing experiment only (RTC_EXPERIMENT): deferred samples neither stored nor summed */
 #else
-#define RTC_AB_NO_SLOTS_ON 0
-#endif
-#ifndef RTC_CHAIN_PRIMF
-#define RTC_CHAIN_PRIMF 1 /* stage the primary filter records in LDS when the block's budget allows */
+constexpr bool kAbNoSlots = false;
 #endif
 extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene, const RtcCamera *cam,
                                      const RtcRenderDesc *d, void *dColors, float *dAccum,
@@ -3442,19 +2412,17 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     /* (a scene without triangles culls too: every tile is then a sky tile) */
     /* the tile cull keeps the workgroup's prefilter survivors in LDS (maskWords u64, <= 48 KB: 393,216 triangles);
      * larger scenes render without it (same frame) */
-    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords <= 6144;
+    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords <= kMaxCullMaskWords;
     /* the split launch (rtc_render_chain + rtc_render_sky): every triangle-only scene */
     const bool fused = cull && !debug && P.sphereCount == 0 && !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
     const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
     const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
     const dim3 superGrid((grid.x + kSuperBlocks - 1) / kSuperBlocks, (grid.y + kSuperBlocks - 1) / kSuperBlocks);
-    const size_t superBytes = RTC_CULL_SUPER ? (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long) : 0;
-    /* (RTC_GEO_CLASSES: a sub-list may receive every tile of a quarter -- all of one class) */
-    const int geoLanes = RTC_GEO_CLASSES || RTC_GEO_HINT ? 4 : kGeoLists; /* (RTC_GEO_HINT: likewise) */
-    const int geoCap = (int)((tiles + geoLanes - 1) / geoLanes * 64);
+    const size_t superBytes = (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long);
+    const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64); /* sub-list l: the tiles t = l mod kGeoLists */
     /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
      * that counts segments joins, the reduction reads the sky kernel's counters) */
-    const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && RTC_SIDE_STREAM && !dSegments;
+    const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && !dSegments;
     const int half = overlap ? s->flip : 0; /* the scratch slot this launch writes */
     P.primF = s->primF + (size_t)half * s->primStride;
     P.primX = s->primX + (size_t)half * s->primStride;
@@ -3463,27 +2431,24 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
      * beside this frame's geometry kernel (round 4: 1/8 share 0.089 -> 0.084 ms); a whole frame keeps them on the
      * launch stream (there the early cull holds CUs the geometry kernel waits for: 0.347 -> 0.361 ms) */
     const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
-    /* RTC_SHARE_CHAIN_CS: an overlapped launch prepares, culls AND runs its geometry kernel on one of two cull streams,
+    /* An overlapped launch prepares, culls AND runs its geometry kernel on one of two cull streams,
      * by slot parity: no cross-stream wait between its cull and its geometry kernel (round 4: ~12 us per 1080p 1/8 share
      * frame), its cull runs beside the previous launch's geometry kernel (on the other stream), and its geometry kernel
      * is not ordered after that one, whose tail it fills.  They share nothing: other scratch slot, counter set and Color
      * buffer, and these launches sum in-kernel (no sample slots, whole frames included).  The previous launch's cull
      * (which zeroes this launch's counter set) is ordered before this one's by its event; `st` waits for the geometry
      * kernel at the end of the launch.  Round 4: 1/8 share 0.087 -> 0.079 ms, whole frame 0.343 -> 0.339 ms
-     * (RTC_ALT_FULL; its tile cull then runs beside the previous frame's kernels, 20 -> ~100 us, off the critical path). */
-#ifndef RTC_ALT_FULL
-#define RTC_ALT_FULL 1 /* whole pipelined frames on the alternating cull streams too */
-#endif
+     * (whole pipelined frames on the alternating streams too; their tile cull then runs beside the previous frame's
+     * kernels, 20 -> ~100 us, off the critical path). */
     /* (whole frames of fewer than kInlineSumPixels pixels keep the launch stream: C1's 256 x 256 x 1 frame took
      * 0.038 -> 0.073 ms on the alternating streams, its period then being cross-stream hops) */
-    const bool chainOnCs = RTC_SHARE_CHAIN_CS && overlap && RTC_CULL_STREAM &&
-                           (smallShare || (RTC_ALT_FULL && (size_t)d->width * (size_t)rows > kInlineSumPixels));
+    const bool chainOnCs = overlap && (smallShare || (size_t)d->width * (size_t)rows > kInlineSumPixels);
     if (chainOnCs && !s->cst2) { /* created on first use: whole frames keep three streams (one more costs them ~1 %) */
         int leastPrio = 0, greatestPrio = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
         HIP_TRY(hipStreamCreateWithPriority(&ms->cst2, hipStreamNonBlocking, greatestPrio));
     }
-    hipStream_t cs = chainOnCs ? ((half & 1) ? s->cst2 : s->cst) : overlap && smallShare && RTC_CULL_STREAM ? s->cst : st;
+    hipStream_t cs = chainOnCs ? ((half & 1) ? s->cst2 : s->cst) : st;
     hipStream_t gs = chainOnCs ? cs : st; /* the geometry kernel's stream */
     /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
      * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
@@ -3567,25 +2532,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
         P.geoList = order + blocks + 4 + kGeoLists * kGeoCountStride;
         P.geoCap = geoCap;
-        P.cullPrio = smallShare && (size_t)d->width * (size_t)rows > (size_t)RTC_CULL_PRIO_MIN_PIXELS;
-        if (RTC_GEO_HINT) { /* grown on demand (hipFree synchronises: no launch still uses the old one) */
-            if (tiles * 64 > s->tileHintCap) {
-                if (ms->tileHint)
-                    HIP_TRY(hipFree(ms->tileHint));
-                ms->tileHint = nullptr;
-                ms->tileHintCap = 0;
-                HIP_TRY(hipMalloc((void **)&ms->tileHint, tiles * 64));
-                HIP_TRY(hipMemset(ms->tileHint, 0, tiles * 64));
-                ms->tileHintCap = tiles * 64;
-            }
-            P.tileHint = s->tileHint;
-        }
+        P.cullPrio = smallShare && (size_t)d->width * (size_t)rows > kCullPrioMinPixels;
         /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
          * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
          * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
          * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
          * 4K 1/8 share are faster deferred) */
-        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !RTC_INLINE_ALL && !chainOnCs) {
+        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !chainOnCs) {
             const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
             const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
             const size_t need = cap * per + 256;
@@ -3623,13 +2576,15 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     /* the previous split launch's tile cull zeroes this launch's counter set (P.geoCountNext): when it ran on another
      * stream (the other cull stream, a cull stream before a launch on `st`, another caller stream), wait for it --
      * evFork is its completion (only split launches record it, and only they touch the counter sets) */
-    if (chain && s->cullStream && s->cullStream != cs)
+    /* (the null stream is a stream like any other here: a previous cull on it is waited for too -- ADVICE r05) */
+    const bool waitPrevCull = chain && s->cullValid && s->cullStream != cs;
+    if (waitPrevCull)
         HIP_TRY(hipStreamWaitEvent(cs, s->evFork, 0));
     const bool prepCurrent =
         s->prepValid[half] && s->prepStream[half] == cs && memcmp(s->prepOrigin[half], org, sizeof org) == 0;
-    /* the previous split launch's cull zeroed this launch's counter set, and `cs` is ordered after it (same stream, or
-     * the evFork wait above) */
-    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || RTC_SIDE_STREAM));
+    /* the previous split launch's cull zeroed this launch's counter set, and `cs` is ordered after it: the same stream,
+     * or the evFork wait above */
+    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || waitPrevCull));
     /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
      * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
     if (chain)
@@ -3656,7 +2611,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     if (cull) {
         /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
         HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), cs,
-                            fused && RTC_SIDE_STREAM ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
+                            fused ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
         if (chain) { /* this cull zeroes the next set's counters (P.geoCountNext) on `cs` */
             ms->geoSeq++;
             ms->cullValid = true;
@@ -3669,33 +2624,25 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         if (fused) {
             /* the split launch: the sky pixels on the side stream, concurrently with rtc_render_chain over the
              * geometry pixels (the tile cull's sub-lists) on `st`; `st` then waits for both */
-            hipStream_t skyStream = RTC_SIDE_STREAM ? s->side : st;
+            hipStream_t skyStream = s->side;
             /* (RTC_F_OVERLAP: the geometry kernel does not wait for the previous launch's sky pass -- in the
              * pipelined steady state it has ended by the time this tile cull does, and the wait was a ~10 us
              * cross-stream hop on every frame; round 2 waited here so that the persistent geometry workgroups
              * found the chip free) */
-            if (RTC_SIDE_STREAM) {
-                HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
-            }
+            HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky0, skyStream));
             const bool skyWide = smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
-            if (RTC_SKY_ROWS && skyWide)
+            if (skyWide)
                 hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0,
                                    skyStream, P, (const unsigned *)tileW);
-            else if (RTC_SKY_ROWS)
-                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, skyStream, P,
-                                   (const unsigned *)tileW);
-            else if (skyWide)
-                hipLaunchKernelGGL(rtc_render_sky<4>, grid, dim3(256), 0, skyStream, P, (const unsigned *)tileW);
             else
-                hipLaunchKernelGGL(rtc_render_sky<1>, dim3(grid.x * 2, grid.y * 2), dim3(64), 0, skyStream, P,
+                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, skyStream, P,
                                    (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky1, skyStream));
-            if (RTC_SIDE_STREAM)
-                HIP_TRY(hipEventRecord(s->evJoin, s->side));
+            HIP_TRY(hipEventRecord(s->evJoin, s->side));
             if (overlap) { /* this sky pass reads scratch slot `half` until evSkyDone[half] (recorded below) */
                 ms->skyPending[half] = true;
                 ms->skyKey[half] = key;
@@ -3708,13 +2655,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : s->chainWgsFull;
             const size_t rec = s->chunkCount <= 1 ? (size_t)soa_slots(s->clusterCount * kClusterSize) * sizeof(DevTri) : 0;
             const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
-            P.chainPrimF = RTC_CHAIN_PRIMF && s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;
+            P.chainPrimF = s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;
             const size_t floorLds = chain_lds_floor(wgsPerCu);
             const size_t dyn = std::max<size_t>(rec + (P.chainPrimF ? pf : 0),
                                                 floorLds > kChainStaticLds ? floorLds - kChainStaticLds : 0);
             /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
              * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
-            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || RTC_AB_NO_SLOTS_ON) ? s->evGeoDone[half] : nullptr;
+            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || kAbNoSlots) ? s->evGeoDone[half] : nullptr;
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, gs, chainStop, P));
@@ -3726,7 +2673,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, gs, chainStop, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, gs));
-            if (P.sampleCap > 0 && !RTC_AB_NO_SLOTS_ON) {
+            if (P.sampleCap > 0 && !kAbNoSlots) {
                 const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
                 HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, gs, overlap ? s->evGeoDone[half] : nullptr,
                                     P));
@@ -3752,8 +2699,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 ms->flip = (ms->flip + 1) % kSkySlots;
                 return 0;
             }
-            if (RTC_SIDE_STREAM)
-                HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
+            HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
             return finish();
         }
         ms->timed = false;
@@ -3857,335 +2803,5 @@ extern "C" int rtc_copy_async(void *dst, const void *src, size_t bytes, int bloc
     hipLaunchKernelGGL(rtc_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        (const unsigned char *)src, (unsigned char *)dst, bytes);
     HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-/* ---- probes: single reference functions on the device, for known-answer tests ---------------------- */
-__global__ void probe_tri_kernel(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst)
-{
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const Ray R = rays[i];
-    const Triangle T = tris[i];
-    const V3 A = v3(T.posA);
-    float d = 0.f;
-    bool h = ray_triangle(v3(R.pos), v3(R.dir), A, sub(v3(T.posB), A), sub(v3(T.posC), A), v3(T.normal), d);
-    didHit[i] = h ? 1 : 0;
-    dst[i] = h ? d : 0.f;
-}
-
-__global__ void probe_sphere_kernel(const Ray *rays, const Sphere *sph, size_t n, int *didHit, float *dst,
-                                    vec3 *normal)
-{
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const Ray R = rays[i];
-    const Sphere S = sph[i];
-    float d = 0.f;
-    bool h = ray_sphere(v3(R.pos), v3(R.dir), v3(S.pos), S.r, d);
-    didHit[i] = h ? 1 : 0;
-    dst[i] = h ? d : 0.f;
-    V3 nrm{0.f, 0.f, 0.f};
-    if (h)
-        nrm = normalized(sub(add(v3(R.pos), mul(v3(R.dir), d)), v3(S.pos)));
-    normal[i] = vec3{nrm.x, nrm.y, nrm.z};
-}
-
-__global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n, vec3 *out)
-{
-    __shared__ PowTablesLds sPow; /* the environment reads its powf tables from LDS, as in the render kernels */
-    sPow.fill(threadIdx.x);
-    __syncthreads();
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    Scene s = scenes[i];
-    EnvParams e{};
-    sPow.attach(e);
-    e.sun = v3(s.normalizedSunDirection);
-    e.horizon = v3(s.skyColorHorizon);
-    e.zenith = v3(s.skyColorZenith);
-    e.ground = v3(s.groundColor);
-    e.focus = s.sunFocus;
-    e.intensity = s.sunIntensity;
-    e.sunSkip = env_sun_skippable(e.focus, e.intensity);
-    V3 c = environment(v3(rays[i].dir), e);
-    out[i] = vec3{c.x, c.y, c.z};
-}
-
-__global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, float *uni, float *nrm, vec3 *dirs)
-{
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    unsigned s = seeds[i];
-    for (int k = 0; k < draws; ++k)
-        uni[i * draws + k] = random_value(s);
-    s = seeds[i];
-    for (int k = 0; k < draws; ++k)
-        nrm[i * draws + k] = random_normal(s);
-    s = seeds[i];
-    for (int k = 0; k < draws; ++k) {
-        V3 d = random_direction(s);
-        dirs[i * draws + k] = vec3{d.x, d.y, d.z};
-    }
-}
-
-/* Cluster culling soundness (DevCluster): every (ray, cluster) pair is culled or not by cluster_culled, and
- * every triangle of the cluster is tested with the reference's rayTriangle arithmetic.  counts: [0] hits in
- * culled clusters (must stay 0), [1] clusters culled, [2] cluster tests, [3] hits, [4] float bits of the
- * largest (distance from the ball centre to the reported hit point) - r over all hits; with reach, [5] hits on
- * records judged unreachable from the ray's origin (aligned_normal; must stay 0), [6] (ray, record) pairs judged
- * so. */
-__global__ void probe_cluster_kernel(const DevTri *clTris, const DevCluster *cl, int clusterCount, int per,
-                                     int recCount, bool reach, const Ray *rays, size_t n,
-                                     unsigned long long *counts)
-{
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const V3 pos = v3(rays[i].pos), dir = v3(rays[i].dir);
-    const float rho = fabsf(dir.x) + fabsf(dir.y) + fabsf(dir.z);
-    unsigned viol = 0, culled = 0, hits = 0, unreachHits = 0, unreach = 0;
-    float excess = 0.f;
-    for (int k = 0; k < clusterCount; ++k) {
-        const DevCluster K = cl[k];
-        const bool cut = rho <= kClusterRhoMax && cluster_culled(pos, dir, rho, dir_dd(dir), K);
-        culled += cut;
-        for (int j = 0; j < per && k * per + j < recCount; ++j) {
-            const DevTri R = clTris[k * per + j];
-            if (__float_as_int(R.pad0) < 0)
-                continue;
-            /* rtc_render_chain's first-bounce reach mask: not hittable from pos in any direction */
-            const V3 q = cross(sub(pos, V3{R.ax, R.ay, R.az}), V3{R.abx, R.aby, R.abz});
-            const bool cannot = reach && rho <= kClusterRhoMax && __float_as_int(R.pad1) != 0 &&
-                                !(dot(V3{R.acx, R.acy, R.acz}, q) > 0.f);
-            unreach += cannot;
-            float dst;
-            if (ray_triangle(pos, dir, V3{R.ax, R.ay, R.az}, V3{R.abx, R.aby, R.abz}, V3{R.acx, R.acy, R.acz},
-                             V3{R.nx, R.ny, R.nz}, dst)) {
-                hits++;
-                viol += cut;
-                unreachHits += cannot;
-                const V3 h = add(pos, mul(dir, dst));
-                const V3 w = sub(h, V3{K.cx, K.cy, K.cz});
-                excess = fmaxf(excess, (float)__builtin_sqrt((double)dot(w, w)) - K.r);
-            }
-        }
-    }
-    atomicAdd(&counts[0], (unsigned long long)viol);
-    atomicAdd(&counts[1], (unsigned long long)culled);
-    atomicAdd(&counts[2], (unsigned long long)clusterCount);
-    atomicAdd(&counts[3], (unsigned long long)hits);
-    atomicMax(&counts[4], (unsigned long long)__float_as_uint(excess));
-    if (reach) {
-        atomicAdd(&counts[5], (unsigned long long)unreachHits);
-        atomicAdd(&counts[6], (unsigned long long)unreach);
-    }
-}
-
-namespace {
-struct Scratch {
-    std::vector<void *> ptrs;
-    ~Scratch()
-    {
-        for (void *p : ptrs)
-            (void)hipFree(p);
-    }
-    hipError_t alloc(void **p, size_t bytes)
-    {
-        hipError_t e = hipMalloc(p, bytes ? bytes : 16);
-        if (e == hipSuccess)
-            ptrs.push_back(*p);
-        return e;
-    }
-};
-int probe_prelude()
-{
-    int n = 0;
-    return rtc_device_count(&n);
-}
-} // namespace
-
-#define ALLOC_IN(dptr, hptr, bytes)                                                                    \
-    HIP_TRY(sc.alloc((void **)&dptr, bytes));                                                          \
-    HIP_TRY(hipMemcpy(dptr, hptr, bytes, hipMemcpyHostToDevice))
-#define ALLOC_OUT(dptr, bytes) HIP_TRY(sc.alloc((void **)&dptr, bytes))
-
-static unsigned probe_blocks(size_t n) { return (unsigned)((n + 255) / 256 > 0 ? (n + 255) / 256 : 1); }
-
-extern "C" int rtc_probe_ray_triangle(const Ray *rays, const Triangle *tris, size_t n, int *didHit, float *dst)
-{
-    if (int rc = probe_prelude())
-        return rc;
-    if (n == 0)
-        return 0;
-    Scratch sc;
-    Ray *dr;
-    Triangle *dt;
-    int *dh;
-    float *dd;
-    ALLOC_IN(dr, rays, n * sizeof(Ray));
-    ALLOC_IN(dt, tris, n * sizeof(Triangle));
-    ALLOC_OUT(dh, n * sizeof(int));
-    ALLOC_OUT(dd, n * sizeof(float));
-    hipLaunchKernelGGL(probe_tri_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, dt, n, dh, dd);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(didHit, dh, n * sizeof(int), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(dst, dd, n * sizeof(float), hipMemcpyDeviceToHost));
-    return 0;
-}
-
-extern "C" int rtc_probe_ray_sphere(const Ray *rays, const Sphere *spheres, size_t n, int *didHit, float *dst,
-                                    vec3 *normal)
-{
-    if (int rc = probe_prelude())
-        return rc;
-    if (n == 0)
-        return 0;
-    Scratch sc;
-    Ray *dr;
-    Sphere *ds;
-    int *dh;
-    float *dd;
-    vec3 *dn;
-    ALLOC_IN(dr, rays, n * sizeof(Ray));
-    ALLOC_IN(ds, spheres, n * sizeof(Sphere));
-    ALLOC_OUT(dh, n * sizeof(int));
-    ALLOC_OUT(dd, n * sizeof(float));
-    ALLOC_OUT(dn, n * sizeof(vec3));
-    hipLaunchKernelGGL(probe_sphere_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dh, dd, dn);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(didHit, dh, n * sizeof(int), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(dst, dd, n * sizeof(float), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(normal, dn, n * sizeof(vec3), hipMemcpyDeviceToHost));
-    return 0;
-}
-
-extern "C" int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *out)
-{
-    if (int rc = probe_prelude())
-        return rc;
-    if (n == 0)
-        return 0;
-    Scratch sc;
-    Ray *dr;
-    Scene *ds;
-    vec3 *dout;
-    ALLOC_IN(dr, rays, n * sizeof(Ray));
-    ALLOC_IN(ds, scenes, n * sizeof(Scene));
-    ALLOC_OUT(dout, n * sizeof(vec3));
-    hipLaunchKernelGGL(probe_env_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dout);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(out, dout, n * sizeof(vec3), hipMemcpyDeviceToHost));
-    return 0;
-}
-
-extern "C" int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
-                                vec3 *direction)
-{
-    if (int rc = probe_prelude())
-        return rc;
-    if (n == 0 || draws <= 0)
-        return 0;
-    Scratch sc;
-    unsigned *dsd;
-    float *du, *dn;
-    vec3 *dd;
-    const size_t m = n * (size_t)draws;
-    ALLOC_IN(dsd, seeds, n * sizeof(unsigned));
-    ALLOC_OUT(du, m * sizeof(float));
-    ALLOC_OUT(dn, m * sizeof(float));
-    ALLOC_OUT(dd, m * sizeof(vec3));
-    hipLaunchKernelGGL(probe_random_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dsd, n, draws, du, dn, dd);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(uniform, du, m * sizeof(float), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(normal, dn, m * sizeof(float), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(direction, dd, m * sizeof(vec3), hipMemcpyDeviceToHost));
-    return 0;
-}
-
-extern "C" int rtc_probe_cluster_bound(const Triangle *tris, int triCount, const Ray *rays, size_t n,
-                                       unsigned long long counts[7])
-{
-    if (!counts || triCount < 0 || (triCount > 0 && !tris) || (n > 0 && !rays))
-        return rtc_fail(RTC_EINVAL, "rtc_probe_cluster_bound: bad argument");
-    memset(counts, 0, 7 * sizeof(unsigned long long));
-    if (int rc = probe_prelude())
-        return rc;
-    if (n == 0 || triCount == 0)
-        return 0;
-    RtcDeviceScene *s = nullptr;
-    if (int rc = rtc_scene_upload(tris, triCount, nullptr, 0, -1, &s))
-        return rc;
-    Scratch sc;
-    Ray *dr = nullptr;
-    unsigned long long *dc = nullptr;
-    int rc = 0;
-    hipError_t e = sc.alloc((void **)&dr, n * sizeof(Ray));
-    if (e == hipSuccess)
-        e = hipMemcpy(dr, rays, n * sizeof(Ray), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = sc.alloc((void **)&dc, 7 * sizeof(unsigned long long));
-    if (e == hipSuccess)
-        e = hipMemset(dc, 0, 7 * sizeof(unsigned long long));
-    if (e == hipSuccess) {
-        /* the clusters, then the chunks (balls over kChunkClusters clusters, rtc_render_chain's first level) */
-        hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->clusters,
-                           s->clusterCount, kClusterSize, s->clusterCount * kClusterSize, true, dr, n, dc);
-        e = hipGetLastError();
-        if (e == hipSuccess && s->chunkCount > 1) {
-            hipLaunchKernelGGL(probe_cluster_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, s->clTris, s->chunks,
-                               s->chunkCount, kClusterSize * kChunkClusters, s->clusterCount * kClusterSize, false, dr, n,
-                               dc);
-            e = hipGetLastError();
-        }
-    }
-    if (e == hipSuccess)
-        e = hipMemcpy(counts, dc, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    if (e != hipSuccess)
-        rc = rtc_fail(-(int)e, "rtc_probe_cluster_bound: %s", hipGetErrorString(e));
-    rtc_scene_release(s);
-    return rc;
-}
-
-extern "C" int rtc_scene_set_geometry_event(RtcDeviceScene *s, void *event)
-{
-    if (!s)
-        return rtc_fail(RTC_EINVAL, "rtc_scene_set_geometry_event: null scene");
-    s->geoEvent = (hipEvent_t)event;
-    return 0;
-}
-
-extern "C" int rtc_scene_set_frame_event(RtcDeviceScene *s, void *event)
-{
-    if (!s)
-        return rtc_fail(RTC_EINVAL, "rtc_scene_set_frame_event: null scene");
-    s->frameEvent = (hipEvent_t)event;
-    return 0;
-}
-
-extern "C" int rtc_scene_set_timing(RtcDeviceScene *s, int enable)
-{
-    if (!s)
-        return rtc_fail(RTC_EINVAL, "rtc_scene_set_timing: null scene");
-    s->timing = enable != 0;
-    return 0;
-}
-
-extern "C" int rtc_scene_kernel_times(const RtcDeviceScene *s, float out[2])
-{
-    if (!s || !out)
-        return rtc_fail(RTC_EINVAL, "rtc_scene_kernel_times: null argument");
-    out[0] = out[1] = -1.f;
-    if (!s->timed)
-        return 0;
-    RtcDeviceGuard guard(s->device);
-    HIP_TRY(hipEventSynchronize(s->evHeavy1));
-    HIP_TRY(hipEventSynchronize(s->evSky1));
-    HIP_TRY(hipEventElapsedTime(&out[0], s->evHeavy0, s->evHeavy1));
-    HIP_TRY(hipEventElapsedTime(&out[1], s->evSky0, s->evSky1));
     return 0;
 }

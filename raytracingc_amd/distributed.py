@@ -95,6 +95,18 @@ def copy_rank_rows_to_host(frame_ptr: int, width: int, height: int, rank: int, w
         copy_rows_d2h_dma(dst + full * world * B * rb, rb, dev_ptr + full * B * rb, rb, rb, tail)
 
 
+def rank_report(local_ms: float, local_segments: int, group=None) -> dict:
+    """What every rank measured, and what the process group itself reports: the backend and the world
+    size of the communicator (on the `nccl` backend: the RCCL communicator's rank count, as torch.distributed reports
+    it), beside each rank's own timed-region ms and segment count, gathered to every rank in rank order."""
+    world = dist.get_world_size(group)
+    got = [None] * world
+    dist.all_gather_object(got, (int(dist.get_rank(group)), float(local_ms), int(local_segments)), group=group)
+    got.sort()
+    return {"backend": str(dist.get_backend(group)), "comm_world_size": int(world),
+            "per_rank_ms": [round(ms, 4) for _, ms, _ in got], "per_rank_segments": [sg for _, _, sg in got]}
+
+
 def rows_per_rank(height: int, world: int, band: int = 1) -> int:
     """Rows in the largest part (rank 0's); every rank's compact buffer is padded to this for the gather."""
     return len(band_rows(height, 0, world, band))

@@ -16,7 +16,7 @@ import torch.multiprocessing as mp
 from conftest import load_tris, setup_from_flags
 
 from raytracingc_amd.distributed import (FrameRenderer, SharedHostFrames, band_rows, interleave_reference,
-                                         rank_config, rows_per_rank)
+                                         rank_config, rank_report, rows_per_rank)
 
 W, H, SPP = 40, 23, 2
 
@@ -232,3 +232,32 @@ def test_gloo_shared_host_frame_rows(world):
     for b in range(2):
         assert np.array_equal(frames[b], full.numpy())
     assert not os.path.exists(f"/dev/shm/{name}")
+
+
+def _report_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = rank_report(0.5 + rank, 1000 + 10 * rank)
+        q.put((rank, rep))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_rank_report_plumbing():
+    """the N > 1 bench line's communicator fields -- the backend, the world size the process group
+    reports (RCCL's on the nccl backend), every rank's ms and segment count in rank order -- identical on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    reps = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {"backend": "gloo", "comm_world_size": 3, "per_rank_ms": [0.5, 1.5, 2.5],
+            "per_rank_segments": [1000, 1010, 1020]}
+    assert all(reps[r] == want for r in range(world))

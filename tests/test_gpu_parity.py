@@ -666,7 +666,12 @@ def test_render_multi_rccl_equals_render(name, band, gpu_available):
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
     assert sa["segments"] == sb["segments"]
     assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
+    assert rt.last_multi_info() == {"path": "host_rows", "devices": rt.device_count(), "comm_ranks": []}
     assert 0 < sa["render_ms"] <= sa["frame_ms"] <= sa["total_ms"]
+    # every communicator of the clique reports the whole clique (ncclCommCount)
+    info = rt.last_multi_info()
+    n = rt.device_count()
+    assert info == {"path": "rccl", "devices": n, "comm_ranks": [n] * n}
 
 
 def test_entry_points_restore_current_device(gpu_available):
@@ -773,6 +778,41 @@ def test_full_size_4k_configs(scene, spp, gpu_available):
     assert sr["segments"] == oseg
     # the whole frame takes the survey's path statistics (~1.03 segments per sample)
     assert 1.0 < s1["segments"] / s1["samples"] < 1.05
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160)], ids=["headline_1080p64", "ns_4k64"])
+def test_whole_frame_bit_exact(W, H, gpu_available):
+    """the ENTIRE metric frame (ultracomplex 1920x1080x64, BASELINE.json `metric`) and the entire NS
+    frame (3840x2160x64) against the CPU oracle rendering every row (oracle/rtc_oracle.c, bit-identical to the
+    reference's own build on every golden fixture): float accumulator bits, Color[] bytes and the traced segment count,
+    all equal.  The frame the bench times (pipelined RTC_F_OVERLAP launches on the cull streams, in-kernel sums) is
+    compared too, byte for byte (main.c:81-104)."""
+    import torch
+
+    tris, tonly = load_tris("ultracomplex")
+    sc, cam, _ = setup_from_flags({})
+    spp = 64
+    c1, a1, s1 = rt.render(tris, None, sc, cam, rt.RenderConfig(W, H, spp, 10, True), want_accum=True)
+    ocol, oacc, oseg = orc.render(tris, None, sc, cam, RtcRenderDesc(W, H, spp, 10, tonly, 0, 1, 0), threads=16)
+    assert oacc.shape == (H, W, 3)
+    mx, over, exact = _compare(a1, oacc)
+    print(f"ultracomplex {W}x{H}x{spp} whole frame: max|d|={mx:.3g} over={over} exact={exact:.7f} "
+          f"segments {s1['segments']} vs {oseg}")
+    assert np.array_equal(_bits(a1), _bits(oacc))
+    assert np.array_equal(c1, ocol)
+    assert s1["segments"] == oseg
+    # the benchmarked launch path: three pipelined frames into three buffers, each equal to the oracle's bytes
+    ds = rt.DeviceScene(tris, None)
+    st = torch.cuda.Stream()
+    bufs = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()
+    for b in bufs:
+        ds.render_rows_async(sc, cam, rt.RenderConfig(W, H, spp, 10, True, overlap=True), b.data_ptr(),
+                             stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for b in bufs:
+        assert np.array_equal(b.cpu().numpy(), ocol)
+    ds.close()
 
 
 def test_overlapped_then_other_launches_same_buffer(gpu_available):
@@ -991,6 +1031,7 @@ def test_render_multi_host_rows_equals_render(name, band, gpu_available):
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
     assert sa["segments"] == sb["segments"]
     assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
+    assert rt.last_multi_info() == {"path": "host_rows", "devices": rt.device_count(), "comm_ranks": []}
 
 
 def test_frame_loop_pipelined_host_frames(gpu_available):
