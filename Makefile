@@ -5,6 +5,7 @@
 
 HIPCC    ?= /opt/rocm/bin/hipcc
 CC       ?= gcc
+CXX      ?= g++
 ARCH     ?= gfx950
 BUILD    := build
 LIBDIR   := raytracingc_amd/_lib
@@ -29,7 +30,7 @@ $(BUILD)/scene_build.o: $(CSRC)/scene_build.c $(CSRC)/rtc_internal.h include/rtc
 	$(CC) $(CFLAGS) -c $< -o $@
 
 # header dependencies: explicit below, and generated (-MMD) for anything the explicit lists miss
-HDRS     := $(CSRC)/rtc_layout.h $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_bm_tables.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h
+HDRS     := $(CSRC)/rtc_layout.h $(CSRC)/rtc_plan.h $(CSRC)/rtc_device.h $(CSRC)/rtc_math.h $(CSRC)/rtc_bm_tables.h $(CSRC)/rtc_hip_util.h $(CSRC)/rtc_internal.h include/rtc.h
 -include $(wildcard $(BUILD)/*.d)
 
 $(BUILD)/rtc_render.o: $(CSRC)/rtc_render.hip $(HDRS) | $(BUILD)
@@ -44,8 +45,12 @@ $(BUILD)/rtc_scene.o: $(CSRC)/rtc_scene.hip $(HDRS) | $(BUILD)
 $(BUILD)/rtc_probe.o: $(CSRC)/rtc_probe.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
 
+# the launch planner: pure host C++ (rtc_plan.h), no HIP
+$(BUILD)/rtc_plan.o: $(CSRC)/rtc_plan.cpp $(CSRC)/rtc_plan.h include/rtc.h | $(BUILD)
+	$(CXX) -std=c++17 -O2 -fPIC -Wall -Wextra -c $< -o $@
+
 # the objects every library variant shares (the render kernels are rtc_render.o, or a variant of it)
-COMMON   := $(BUILD)/rtc_frame.o $(BUILD)/rtc_scene.o $(BUILD)/rtc_probe.o $(BUILD)/scene_build.o
+COMMON   := $(BUILD)/rtc_frame.o $(BUILD)/rtc_scene.o $(BUILD)/rtc_probe.o $(BUILD)/rtc_plan.o $(BUILD)/scene_build.o
 
 $(LIB): $(BUILD)/rtc_render.o $(COMMON)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -Wl,-soname,librtc.so -ldl -L/opt/rocm/lib -lhsa-runtime64

@@ -256,6 +256,22 @@ int rtc_copy_rows_d2h_dma(void *hostDst, size_t hostPitch, const void *devSrc, s
 int rtc_host_register(void *p, size_t bytes);
 int rtc_host_unregister(void *p);
 
+/* Test hooks of the launch planner (rtc_plan.h; no GPU involved): the ordering decisions rtc_render_rows_async would take
+ * for a sequence of launches on a scene of triCount triangles, without any device.  rtc_plan_sim_launch plans one launch
+ * (d; the caller's stream identity `stream`, 0 = the null stream; Color / accumulator buffer identities; segment counters
+ * asked for or not; the camera cam[13] = origin, ex, ey, ez, fov and environment env[14] = sun, horizon, zenith, ground,
+ * focus, intensity that decide the pixel values) and writes its operations as 4 ints each (kind 0 kernel / 1 record /
+ * 2 wait, stream 0 caller / 1, 2 cull streams / 3 side stream, event, kernel) and each kernel's memory footprint as 6 u64
+ * each (op index, resource, access, id, byte range), then one u64 record (~0, scratch regrown, slot, alternating streams,
+ * overlapped, slot offset).  Returns nOps | (footprint records << 8).  legacySlotLayout: round 5's broken scratch
+ * layout (slot h at h x the launch's own slot size), for the test that must catch it. */
+typedef struct RtcPlanSim RtcPlanSim;
+int rtc_plan_sim_create(int triCount, int legacySlotLayout, RtcPlanSim **out);
+int rtc_plan_sim_launch(RtcPlanSim *sim, const RtcRenderDesc *d, unsigned long long stream, unsigned long long colors,
+                        unsigned long long accum, int segments, const float cam[13], const float env[14], int *ops,
+                        int maxOps, unsigned long long *footprint, int maxFootprint);
+int rtc_plan_sim_release(RtcPlanSim *sim);
+
 /* Pipelined frames on one device, driven from native code (the per-frame host cost is the launch enqueue alone).
  * Frame k renders d's rows with RTC_F_OVERLAP into devRows[k % nbuf] (device buffers of rows_selected*width*3 bytes)
  * on `stream`; a copy thread waits for the frame's event and moves the rows into hostRows[k % nbuf] (page-locked,

@@ -139,7 +139,7 @@ EXPORTS = [
     "rtc_bounce_hit_share", "rtc_scene_chain_wgs",
     "rtc_scene_set_geometry_event", "rtc_scene_set_frame_event",
     "rtc_deinterleave_async", "rtc_deinterleave_bands_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
-    "rtc_host_unregister", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
+    "rtc_host_unregister", "rtc_plan_sim_create", "rtc_plan_sim_launch", "rtc_plan_sim_release", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
     "rtc_probe_cluster_bound",
 ]
@@ -204,6 +204,10 @@ def lib() -> C.CDLL:
                                  ip, vp, C.POINTER(RtcLoopStats)]
     L.rtc_frame_loop_cameras.argtypes = [vp, C.POINTER(Scene), vp, ip, C.POINTER(RtcRenderDesc), vp, vp, sz, ip, ip,
                                          vp, C.POINTER(RtcLoopStats)]
+    L.rtc_plan_sim_create.argtypes = [ip, ip, C.POINTER(vp)]
+    L.rtc_plan_sim_launch.argtypes = [vp, C.POINTER(RtcRenderDesc), C.c_ulonglong, C.c_ulonglong, C.c_ulonglong, ip, vp,
+                                      vp, vp, ip, vp, ip]
+    L.rtc_plan_sim_release.argtypes = [vp]
     L.rtc_dma_pending.argtypes = [vp, sz]
     L.rtc_dma_debug_inflight.argtypes = [vp, sz, ip]
     L.rtc_rows_selected.argtypes = [C.POINTER(RtcRenderDesc)]

@@ -9,6 +9,7 @@
 
 #include "../../include/rtc.h"
 #include "rtc_device.h"
+#include "rtc_plan.h"
 
 using namespace rtcdev;
 
@@ -99,11 +100,9 @@ constexpr double kWgsHitShare = 0.15;
 constexpr int kGeoLists = 16, kGeoCountStride = 32;
 constexpr int kGeoRing = 16, kGeoSetInts = kGeoLists * kGeoCountStride;
 static_assert(kGeoSetInts >= kGeoLists * kGeoCountStride, "a counter set holds every sub-list counter");
-struct SkyKey {
-    const void *colors, *accum;
-    float cam[13], env[14];
-    int dims[9];
-};
+static_assert(kSkySlots == rtcplan::kSlots && kGeoRing == rtcplan::kGeoRing && kGeoLists == rtcplan::kGeoLists &&
+                  kGeoCountStride == rtcplan::kGeoCountStride,
+              "the planner's slot and counter-set layout is the device's");
 struct RtcDeviceScene {
     int device;
     int cuCount; /* compute units of the device (the persistent chain kernel's workgroups are a multiple of it) */
@@ -122,55 +121,38 @@ struct RtcDeviceScene {
     DevPrimF *primF;
     DevPrimX *primX;
     size_t primStride;
-    /* per-launch scratch (rtc_tile_cull / rtc_order_blocks): the candidate bit-sets (maskWords u64 per 8x8
-     * tile), the per-workgroup weights and the workgroup dispatch order; grown on demand */
+    /* per-launch scratch (rtc_tile_cull / rtc_order_blocks): kSkySlots slots of the candidate bit-sets, pixel masks,
+     * weights, dispatch order, geometry-pixel sub-lists and superblock survivors (rtcplan::Layout); grown on demand
+     * (plan.scratchCap bytes) */
     unsigned char *scratch;
-    size_t scratchCap; /* bytes */
-    /* RTC_F_OVERLAP: launches cycle through kSkySlots slots of the scratch; skyPending[h]: a sky pass that reads
-     * slot h has not been joined into a launch stream yet (evSkyDone[h] fires when it ends; skyKey[h]: the rows,
-     * camera and environment it writes; skySeq[h]: its enqueue order) */
-    int flip;
     /* rtc_render_chain's sub-list counters: a ring of kGeoRing sets, set q % kGeoRing for the q-th split launch;
-     * each launch's tile cull zeroes the next launch's set, so a launch on the same stream as the previous one
-     * needs no rtc_prep_primary to clear its counters (cullStream: that stream) */
+     * each launch's tile cull zeroes the next launch's set */
     int *geoCounts;
-    unsigned long long geoSeq;
-    hipStream_t cullStream;
-    bool cullValid;
     double hitShare;  /* bounce_hit_share at upload */
     int chainWgsFull; /* rtc_render_chain workgroups per CU for whole frames */
-    /* rtc_prep_primary's records of slot h are for prepOrigin[h], written on prepStream[h] (prepValid[h]: they exist) */
-    bool prepValid[kSkySlots];
-    float prepOrigin[kSkySlots][3];
-    hipStream_t prepStream[kSkySlots];
-    /* RTC_F_OVERLAP launches prepare and cull on `cst` (a high-priority stream of the scene): the next frame's tile
-     * cull then runs while this frame's geometry kernel still runs, instead of after it on the launch stream.
-     * slotUsed[h]: an overlapped launch used slot h (its sky pass ends at evSkyDone[h], its launch-stream kernels at
-     * evGeoDone[h]: a later launch's cull waits for both before rewriting the slot) */
+    /* every ordering decision's state: slots, pending sky passes, counter sets, prep records (rtc_plan.h) */
+    rtcplan::State plan;
+    /* streams: overlapped launches prepare, cull and run their geometry kernel on `cst` or `cst2` (high priority, by
+     * slot parity); the sky pass runs on `side` (low priority) */
     hipStream_t cst;
     hipStream_t cst2; /* the second cull stream (odd slots; created on first use) */
-    bool slotUsed[kSkySlots];
-    hipEvent_t evCullSync; /* the launch stream's position when the culls move to `cst` */
-    bool skyPending[kSkySlots];
-    SkyKey skyKey[kSkySlots];
-    unsigned long long skySeq[kSkySlots], skyCount; /* enqueue order of the sky passes (skySeq[h] of slot h's) */
+    hipStream_t side;
+    /* the scene's ordering events (rtcplan::Event): the caller stream's position when the culls move to a cull stream,
+     * the tile cull's completion (the sky pass forks there), the sky pass's end, and per slot the end of its launch's
+     * sky pass (after its geometry kernel) and of its geometry kernel */
+    hipEvent_t evCullSync, evFork, evJoin;
     hipEvent_t evSkyDone[kSkySlots], evGeoDone[kSkySlots];
     hipEvent_t frameEvent; /* caller's (rtc_scene_set_frame_event) or null */
-    /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel, summed in
-     * sample order at the kernel's end by the wave that rendered the pixel (grown on demand, <= kSampleBufBudget
-     * bytes) */
-    unsigned char *samples;
-    size_t samplesCap; /* bytes */
-    int maskWords;     /* ceil(triPadded / 64) */
-    unsigned long long *segSlots; /* per-launch partial segment counters */
-    /* the split launch runs the sky kernel on `side`, concurrently with the heavy-tile kernel */
-    hipStream_t side;
-    hipEvent_t evFork, evJoin;
-    /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
-    hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
     /* caller's event (rtc_scene_set_geometry_event): recorded on the caller's stream once a launch's
      * geometry-pixel kernels are enqueued (before the join with the sky pass); null: none */
     hipEvent_t geoEvent;
+    /* rtc_render_chain's deferred accumulation: the accumulated samples' radiance per geometry pixel (grown on demand,
+     * <= kSampleBufBudget bytes: plan.samplesCap) */
+    unsigned char *samples;
+    int maskWords;     /* ceil(triPadded / 64) */
+    unsigned long long *segSlots; /* per-launch partial segment counters */
+    /* timing events around the split launch's two kernels (rtc_scene_kernel_times) */
+    hipEvent_t evHeavy0, evHeavy1, evSky0, evSky1;
     bool timing; /* record them (rtc_scene_set_timing; off by default: each record costs the launch a few us) */
     bool timed;  /* the last launch was a split launch that recorded them */
 };

@@ -846,7 +846,7 @@ __device__ bool tile_prunes(const TileCone &K, const DevPrimF &F)
  * skips its own double-precision cone.  Same candidate lists bit for bit (each level only removes triangles the
  * per-pixel filter rejects for every pixel of the rectangle). */
 constexpr int kSuperBlocks = 4;
-constexpr size_t kSuperCullPixels = 400000; /* launches of more pixels run level 0 */
+/* (launches of more than rtcplan::kSuperCullPixels pixels run level 0) */
 __global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned long long *__restrict__ superMask)
 {
     const int sx = blockIdx.x, sy = blockIdx.y, lane = threadIdx.x;
@@ -1390,15 +1390,11 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
  * window.  The lanes of a wave share the pixel's primary ray: the primary trace is wave-uniform (scalar-loaded
  * candidate records), the shading at the primary hit runs in lockstep, and only the bounce segments diverge.
  * Work: one wave per geometry pixel, from the tile cull's sub-lists (see the kernel). */
-constexpr size_t kSampleBufBudget = (size_t)2 << 30; /* bytes of HBM for the deferred accumulation slots */
-/* Shares (row stride > 1) of up to this many pixels are "small": they sum in-kernel, run 4 chain workgroups per CU and,
+static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner sizes the deferred sample slots");
+/* Shares (row stride > 1) of up to rtcplan::kInlineSumPixels pixels are "small": they sum in-kernel and,
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
-#ifndef RTC_INLINE_SUM_PIXELS
-#define RTC_INLINE_SUM_PIXELS 600000
-#endif
-constexpr size_t kInlineSumPixels = RTC_INLINE_SUM_PIXELS;
 constexpr int kChainBlock = 256; /* threads per chain workgroup (two-wave workgroups were slower everywhere, r04_ze) */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
@@ -2294,12 +2290,13 @@ static hipError_t launch_stop(void (*k)(K...), dim3 g, dim3 b, size_t sh, hipStr
     return hipGetLastError();
 }
 
-static SkyKey sky_key(const RenderParams &P)
+/* what an unjoined sky pass writes (rtcplan::Key): its buffers and everything that decides their values */
+static rtcplan::Key sky_key(const RenderParams &P)
 {
-    SkyKey k;
+    rtcplan::Key k;
     memset(&k, 0, sizeof k);
-    k.colors = P.colors;
-    k.accum = P.accum;
+    k.colors = (uint64_t)(uintptr_t)P.colors;
+    k.accum = (uint64_t)(uintptr_t)P.accum;
     const V3 c[4] = {P.origin, P.ex, P.ey, P.ez}, e[4] = {P.env.sun, P.env.horizon, P.env.zenith, P.env.ground};
     for (int i = 0; i < 4; ++i) {
         k.cam[3 * i] = c[i].x, k.cam[3 * i + 1] = c[i].y, k.cam[3 * i + 2] = c[i].z;
@@ -2402,320 +2399,204 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.ez = v3(cam->ez);
     P.fov = cam->fov;
     P.env = env_of(*scene);
-    dim3 grid((d->width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
     hipStream_t st = (hipStream_t)stream;
-    /* (P.primF / P.primX: the scratch slot's copy, below) */
-    /* tile candidate lists (one bit-set per 8x8 tile, 4 per workgroup), workgroup and tile weights and the
-     * dispatch order, in one scratch buffer grown on demand (hipFree synchronises, so a previous launch still
-     * reading the old buffer has finished) */
-    const bool debug = (d->flags & RTC_F_DEBUG_BOUNCES) != 0;
-    /* (a scene without triangles culls too: every tile is then a sky tile) */
-    /* the tile cull keeps the workgroup's prefilter survivors in LDS (maskWords u64, <= 48 KB: 393,216 triangles);
-     * larger scenes render without it (same frame) */
-    const bool cull = !(d->flags & RTC_F_NO_TILE_CULL) && s->maskWords <= kMaxCullMaskWords;
-    /* the split launch (rtc_render_chain + rtc_render_sky): every triangle-only scene */
-    const bool fused = cull && !debug && P.sphereCount == 0 && !(d->flags & (RTC_F_NO_COOP | RTC_F_NO_REORDER));
-    const size_t blocks = (size_t)grid.x * grid.y, tiles = 4 * blocks;
-    const size_t maskBytes = tiles * (size_t)s->maskWords * sizeof(unsigned long long);
-    const dim3 superGrid((grid.x + kSuperBlocks - 1) / kSuperBlocks, (grid.y + kSuperBlocks - 1) / kSuperBlocks);
-    const size_t superBytes = (size_t)superGrid.x * superGrid.y * s->maskWords * sizeof(unsigned long long);
-    const int geoCap = (int)((tiles + kGeoLists - 1) / kGeoLists * 64); /* sub-list l: the tiles t = l mod kGeoLists */
-    /* RTC_F_OVERLAP: the sky pass is not joined into `st` (the split launch on the side stream only; a launch
-     * that counts segments joins, the reduction reads the sky kernel's counters) */
-    const bool overlap = (d->flags & RTC_F_OVERLAP) && fused && !dSegments;
-    const int half = overlap ? s->flip : 0; /* the scratch slot this launch writes */
-    P.primF = s->primF + (size_t)half * s->primStride;
-    P.primX = s->primX + (size_t)half * s->primStride;
-    /* the stream of the preparation and the culls: for an overlapped small share (the 1080p frame's 1/8, whose
-     * geometry kernel is the critical path) the scene's high-priority cull stream, so the next frame's cull runs
-     * beside this frame's geometry kernel (round 4: 1/8 share 0.089 -> 0.084 ms); a whole frame keeps them on the
-     * launch stream (there the early cull holds CUs the geometry kernel waits for: 0.347 -> 0.361 ms) */
-    const bool smallShare = d->rowStride > 1 && (size_t)d->width * (size_t)rows <= kInlineSumPixels;
-    /* An overlapped launch prepares, culls AND runs its geometry kernel on one of two cull streams,
-     * by slot parity: no cross-stream wait between its cull and its geometry kernel (round 4: ~12 us per 1080p 1/8 share
-     * frame), its cull runs beside the previous launch's geometry kernel (on the other stream), and its geometry kernel
-     * is not ordered after that one, whose tail it fills.  They share nothing: other scratch slot, counter set and Color
-     * buffer, and these launches sum in-kernel (no sample slots, whole frames included).  The previous launch's cull
-     * (which zeroes this launch's counter set) is ordered before this one's by its event; `st` waits for the geometry
-     * kernel at the end of the launch.  Round 4: 1/8 share 0.087 -> 0.079 ms, whole frame 0.343 -> 0.339 ms
-     * (whole pipelined frames on the alternating streams too; their tile cull then runs beside the previous frame's
-     * kernels, 20 -> ~100 us, off the critical path). */
-    /* (whole frames of fewer than kInlineSumPixels pixels keep the launch stream: C1's 256 x 256 x 1 frame took
-     * 0.038 -> 0.073 ms on the alternating streams, its period then being cross-stream hops) */
-    const bool chainOnCs = overlap && (smallShare || (size_t)d->width * (size_t)rows > kInlineSumPixels);
-    if (chainOnCs && !s->cst2) { /* created on first use: whole frames keep three streams (one more costs them ~1 %) */
+    /* every ordering decision -- slot, streams, events, which kernels -- comes from the planner (rtc_plan.h); this
+     * function executes its operations */
+    rtcplan::Request rq{};
+    rq.stream = (uint64_t)(uintptr_t)st;
+    rq.flags = d->flags;
+    rq.width = d->width;
+    rq.rows = rows;
+    rq.rowStride = d->rowStride;
+    rq.spp = d->spp;
+    rq.sphereCount = P.sphereCount;
+    rq.triPadded = s->triPadded;
+    rq.maskWords = s->maskWords;
+    rq.segments = dSegments != nullptr;
+    rq.key = sky_key(P);
+    memcpy(rq.origin, &P.origin, sizeof rq.origin);
+    static thread_local rtcplan::Plan pl;
+    rtcplan::plan_launch(s->plan, rq, pl);
+    /* the saved state claims only what has been enqueued: until every operation below is, a later launch sees none of
+     * this launch's primary records or counter zeroing (it re-runs rtc_prep_primary) */
+    ms->plan.prepValid[pl.half] = false;
+    ms->plan.cullValid = false;
+    if (pl.needCst2) { /* created on first use: whole frames keep three streams (one more costs them ~1 %) */
         int leastPrio = 0, greatestPrio = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
         HIP_TRY(hipStreamCreateWithPriority(&ms->cst2, hipStreamNonBlocking, greatestPrio));
+        ms->plan.cst2 = true;
     }
-    hipStream_t cs = chainOnCs ? ((half & 1) ? s->cst2 : s->cst) : st;
-    hipStream_t gs = chainOnCs ? cs : st; /* the geometry kernel's stream */
-    /* An unjoined sky pass of an earlier RTC_F_OVERLAP launch may still be writing Color rows and reading its
-     * scratch slot.  A launch that is not itself overlapped waits for every such pass before its first kernel:
-     * whatever its kernels (debug, spheres, brute force, another buffer or camera) they then never race it.  An
-     * overlapped launch waits when a pending pass reads the slot it rewrites, or writes the same Color or
-     * accumulator buffer with other rows, camera or environment (the same ones write the same sky pixels with the
-     * same values, and never a pixel this launch's geometry kernel writes).  One wait, on the newest such pass,
-     * covers every earlier one (the side stream runs them in order), so with kSkySlots slots a pipelined sequence of
-     * one camera waits once every kSkySlots - 1 launches: each wait is a cross-stream hop of ~10 us before the next
-     * kernel (round 3: waiting before every geometry kernel cost 0.107 vs 0.098 ms per 1080p 1/8 share).  Round 4
-     * waits for the newest CONFLICTING pass, not the newest pass: a moving camera's pipelined frames into three
-     * buffers conflict with the pass three launches back, long finished, and no longer wait for the previous frame's
-     * sky pass (which serialised them behind it). */
-    const SkyKey key = sky_key(P);
-    int waitSky = -1; /* the newest pending pass this launch must wait for */
-    for (int h = 0; h < kSkySlots; ++h)
-        if (s->skyPending[h] && /* (with `cs` the cull stream waits for the pass reading its slot itself, below) */
-            (!overlap || (h == half && cs == st) ||
-             ((s->skyKey[h].colors == key.colors || (key.accum && s->skyKey[h].accum == key.accum)) &&
-              memcmp(&s->skyKey[h], &key, sizeof key) != 0)) &&
-            (waitSky < 0 || s->skySeq[h] > s->skySeq[waitSky]))
-            waitSky = h;
-    if (waitSky >= 0) {
-        /* evSkyDone[h] fires once launch h's sky pass AND its geometry kernel have ended (the side stream records it
-         * after waiting for evGeoDone[h]); `cs` inherits this wait through the caller-position event below */
-        HIP_TRY(hipStreamWaitEvent(st, s->evSkyDone[waitSky], 0));
-        const unsigned long long upTo = s->skySeq[waitSky];
-        for (int h = 0; h < kSkySlots; ++h) /* that pass and every earlier one are done before this launch's kernels */
-            if (s->skySeq[h] <= upTo)
-                ms->skyPending[h] = false;
+    if (pl.scratchGrow) { /* every slot (hipFree synchronises the device: no launch still reads the old scratch) */
+        if (ms->scratch)
+            HIP_TRY(hipFree(ms->scratch));
+        ms->scratch = nullptr;
+        ms->plan.scratchCap = 0;
+        HIP_TRY(hipMalloc(&ms->scratch, pl.scratchNeed));
+        ms->plan.scratchCap = pl.scratchNeed;
     }
-    size_t halfBytes = 0;
-    if (cull) {
-        const size_t need = maskBytes + tiles * sizeof(unsigned long long) + (blocks + tiles + blocks + 4) * sizeof(int) +
-                            (kGeoLists * kGeoCountStride + (size_t)kGeoLists * geoCap) * sizeof(int) + /* + sub-lists */
-                            8 + superBytes; /* + the superblock survivors (8-byte aligned) */
-        halfBytes = (need + 255) & ~(size_t)255;
-        if (kSkySlots * halfBytes > s->scratchCap) { /* every slot (hipFree synchronises the device: no pass reads them) */
-            if (ms->scratch)
-                HIP_TRY(hipFree(ms->scratch));
-            ms->scratch = nullptr;
-            ms->scratchCap = 0;
-            HIP_TRY(hipMalloc(&ms->scratch, kSkySlots * halfBytes));
-            ms->scratchCap = kSkySlots * halfBytes;
-        }
+    if (pl.samplesGrow) {
+        if (ms->samples)
+            HIP_TRY(hipFree(ms->samples));
+        ms->samples = nullptr;
+        ms->plan.samplesCap = 0;
+        HIP_TRY(hipMalloc(&ms->samples, pl.samplesNeed));
+        ms->plan.samplesCap = pl.samplesNeed;
     }
-    P.blocksX = (int)grid.x;
-    /* (the counter slots are zero here: rtc_scene_upload clears them, rtc_reduce_segments re-zeroes them) */
-    bool geoRecorded = false;
-    auto finish = [&]() -> int {
-        if (geoEvent && !geoRecorded)
-            HIP_TRY(hipEventRecord(geoEvent, st));
-        if (dSegments) {
-            hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, st, s->segSlots, dSegments);
-            HIP_TRY(hipGetLastError());
-        }
-        if (frameEvent) /* the whole frame is written once `st` reaches here (joined launches) */
-            HIP_TRY(hipEventRecord(frameEvent, st));
-        return 0;
-    };
-    const bool chain = fused;
-    /* slot `half` starts at half x (the allocation's slot size), not half x this launch's size: consecutive launches of
-     * different sizes (the last, shorter row share of a band partition, a whole frame after a share) are in flight
-     * together on the alternating streams, and with per-launch offsets a smaller launch's slot 1 overlapped the
-     * previous launch's slot 0 -- its tile cull overwrote the geometry list that launch's geometry kernel was reading
-     * (geometry pixels left unrendered; found by test_small_shares_sum_in_kernel[True-8-8], round 5) */
-    const size_t slotBytes = s->scratchCap / kSkySlots;
-    unsigned long long *mask = cull ? (unsigned long long *)(s->scratch + (size_t)half * slotBytes) : nullptr;
-    unsigned long long *pixMask = cull ? mask + tiles * (size_t)s->maskWords : nullptr;
-    unsigned *weight = cull ? (unsigned *)(pixMask + tiles) : nullptr;
-    unsigned *tileW = cull ? weight + blocks : nullptr;
-    int *order = cull ? (int *)(tileW + tiles) : nullptr;
-    unsigned long long *superMask = nullptr;
-    if (cull && superBytes) { /* after the sub-lists, 8-byte aligned */
-        const size_t off = ((size_t)((const unsigned char *)(order + blocks + 4 + kGeoLists * kGeoCountStride +
-                                                             (size_t)kGeoLists * geoCap) - s->scratch) + 7) & ~(size_t)7;
-        superMask = (unsigned long long *)(s->scratch + off);
-    }
-    if (chain) {
-        P.geoCount = s->geoCounts + (size_t)(s->geoSeq % kGeoRing) * kGeoSetInts;
-        P.geoCountNext = s->geoCounts + (size_t)((s->geoSeq + 1) % kGeoRing) * kGeoSetInts;
-        P.geoList = order + blocks + 4 + kGeoLists * kGeoCountStride;
-        P.geoCap = geoCap;
-        P.cullPrio = smallShare && (size_t)d->width * (size_t)rows > kCullPrioMinPixels;
-        /* deferred accumulation slots: one per possible geometry pixel of the launch, within the byte budget
-         * (pixels beyond it are accumulated inside rtc_render_chain; same result).  A small share of a row-partitioned
-         * frame sums in the kernel: its in-order pass would be a fixed cost on the frame's critical path (1080p x64
-         * 1/8 share, 135 rows: 0.114 -> 0.108 ms per pipelined frame; at 1/4 the two are equal, whole frames and the
-         * 4K 1/8 share are faster deferred) */
-        if (d->spp > 0 && !(d->flags & RTC_F_CHAIN_INLINE) && !smallShare && !chainOnCs) {
-            const size_t per = (size_t)d->spp * sizeof(SampleSlot) + sizeof(int);
-            const size_t cap = std::min<size_t>((size_t)d->width * (size_t)rows, kSampleBufBudget / per);
-            const size_t need = cap * per + 256;
-            if (need > s->samplesCap) {
-                if (ms->samples)
-                    HIP_TRY(hipFree(ms->samples));
-                ms->samples = nullptr;
-                ms->samplesCap = 0;
-                HIP_TRY(hipMalloc(&ms->samples, need));
-                ms->samplesCap = need;
-            }
-            P.sampleBuf = (SampleSlot *)s->samples;
-            P.itemPix = (int *)(s->samples + cap * (size_t)d->spp * sizeof(SampleSlot));
-            P.sampleCap = (int)cap;
-        }
-    }
-    /* rtc_prep_primary: the primary records of this camera origin, and this launch's sub-list counters zeroed.  It
-     * is skipped when the records are already those of this origin (written on this stream) and the counters were
-     * zeroed by the previous split launch's tile cull on this stream -- frames of one camera position (round 3:
-     * a 5 us kernel at the head of every frame) */
-    const float org[3] = {P.origin.x, P.origin.y, P.origin.z};
-    if (cs != st) {
-        /* The cull stream runs this launch's first kernels, so it starts after everything the caller enqueued on `st`
-         * before the launch (e.g. a wait for the previous consumer of this Color buffer) and after the sky waits above:
-         * an event at `st`'s current position.  `st` carries nothing of earlier launches on the cull streams (they do
-         * not make it wait for their geometry kernels), so this orders no geometry kernel after another.  Then slot
-         * `half`: the earlier launch that used it must have ended (its sky pass and geometry kernel) */
-        HIP_TRY(hipEventRecord(s->evCullSync, st));
-        HIP_TRY(hipStreamWaitEvent(cs, s->evCullSync, 0));
-        if (s->slotUsed[half]) {
-            HIP_TRY(hipStreamWaitEvent(cs, s->evSkyDone[half], 0));
-            HIP_TRY(hipStreamWaitEvent(cs, s->evGeoDone[half], 0));
-        }
-    }
-    /* the previous split launch's tile cull zeroes this launch's counter set (P.geoCountNext): when it ran on another
-     * stream (the other cull stream, a cull stream before a launch on `st`, another caller stream), wait for it --
-     * evFork is its completion (only split launches record it, and only they touch the counter sets) */
-    /* (the null stream is a stream like any other here: a previous cull on it is waited for too -- ADVICE r05) */
-    const bool waitPrevCull = chain && s->cullValid && s->cullStream != cs;
-    if (waitPrevCull)
-        HIP_TRY(hipStreamWaitEvent(cs, s->evFork, 0));
-    const bool prepCurrent =
-        s->prepValid[half] && s->prepStream[half] == cs && memcmp(s->prepOrigin[half], org, sizeof org) == 0;
-    /* the previous split launch's cull zeroed this launch's counter set, and `cs` is ordered after it: the same stream,
-     * or the evFork wait above */
-    const bool countsZeroed = !chain || (s->cullValid && (s->cullStream == cs || waitPrevCull));
-    /* the saved state claims only what has been enqueued: cleared first, set again once its kernel is enqueued (an
-     * early return in between leaves it cleared, and the next launch runs rtc_prep_primary) */
-    if (chain)
-        ms->cullValid = false;
-    if ((s->triPadded > 0 || chain) && !(prepCurrent && countsZeroed)) {
-        ms->prepValid[half] = false;
-        hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, cs, s->tris,
-                           const_cast<DevPrimF *>(P.primF), const_cast<DevPrimX *>(P.primX),
-                           s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, chain ? P.geoCount : nullptr);
-        HIP_TRY(hipGetLastError());
-        ms->prepValid[half] = true;
-        ms->prepStream[half] = cs;
-        memcpy(ms->prepOrigin[half], org, sizeof org);
-    }
-    /* level 0 pays for its extra launch on large frames only (1080p: -7 us per frame); a small share (the 1/8 of a
-     * row-partitioned 1080p frame) culls faster without it (round 4 A/B: 0.111 vs 0.118 ms per joined share) */
-    const bool superCull = (size_t)d->width * (size_t)rows > kSuperCullPixels;
-    if (cull && superMask && superCull && s->maskWords > 0) {
-        P.superMask = superMask;
-        P.superX = (int)superGrid.x;
-        hipLaunchKernelGGL(rtc_super_cull, superGrid, dim3(64), 0, cs, P, superMask);
-        HIP_TRY(hipGetLastError());
-    }
-    if (cull) {
-        /* the split launch forks its sky pass at the tile cull's end: the fork event is the cull's own completion */
-        HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), cs,
-                            fused ? s->evFork : nullptr, P, mask, weight, tileW, pixMask));
-        if (chain) { /* this cull zeroes the next set's counters (P.geoCountNext) on `cs` */
-            ms->geoSeq++;
-            ms->cullValid = true;
-            ms->cullStream = cs;
-        }
-        if (cs != st && !chainOnCs) /* the geometry kernel after the cull */
-            HIP_TRY(hipStreamWaitEvent(st, s->evFork, 0));
+    const int half = pl.half;
+    P.primF = s->primF + (size_t)half * s->primStride;
+    P.primX = s->primX + (size_t)half * s->primStride;
+    P.blocksX = (int)pl.gridX;
+    unsigned long long *mask = nullptr, *pixMask = nullptr, *superMask = nullptr;
+    unsigned *weight = nullptr, *tileW = nullptr;
+    int *order = nullptr;
+    if (pl.cull) {
+        unsigned char *slot = s->scratch + pl.slotOffset;
+        mask = (unsigned long long *)(slot + pl.lay.mask);
+        pixMask = (unsigned long long *)(slot + pl.lay.pixMask);
+        weight = (unsigned *)(slot + pl.lay.weight);
+        tileW = (unsigned *)(slot + pl.lay.tileW);
+        order = (int *)(slot + pl.lay.order);
+        superMask = (unsigned long long *)(slot + pl.lay.superMask);
         P.tileMask = mask;
         P.pixMask = pixMask;
-        if (fused) {
-            /* the split launch: the sky pixels on the side stream, concurrently with rtc_render_chain over the
-             * geometry pixels (the tile cull's sub-lists) on `st`; `st` then waits for both */
-            hipStream_t skyStream = s->side;
-            /* (RTC_F_OVERLAP: the geometry kernel does not wait for the previous launch's sky pass -- in the
-             * pipelined steady state it has ended by the time this tile cull does, and the wait was a ~10 us
-             * cross-stream hop on every frame; round 2 waited here so that the persistent geometry workgroups
-             * found the chip free) */
-            HIP_TRY(hipStreamWaitEvent(s->side, s->evFork, 0));
+        if (!pl.fused)
+            P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
+    }
+    if (pl.superCull) {
+        P.superMask = superMask;
+        P.superX = (int)pl.superX;
+    }
+    if (pl.chain) {
+        P.geoCount = s->geoCounts + (size_t)pl.geoSet * kGeoSetInts;
+        P.geoCountNext = s->geoCounts + (size_t)pl.geoSetNext * kGeoSetInts;
+        P.geoList = (int *)(s->scratch + pl.slotOffset + pl.lay.geoList);
+        P.geoCap = pl.geoCap;
+        P.cullPrio = pl.cullPrio;
+        if (pl.sampleCap > 0) {
+            P.sampleBuf = (SampleSlot *)s->samples;
+            P.itemPix = (int *)(s->samples + (size_t)pl.sampleCap * (size_t)d->spp * sizeof(SampleSlot));
+            P.sampleCap = pl.sampleCap;
+        }
+    }
+    /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary filter records
+     * when the block stays within its workgroups per CU */
+    const int wgsPerCu = pl.smallShare ? RTC_CHAIN_WGS_SHARE : s->chainWgsFull;
+    const size_t recLds = s->chunkCount <= 1 ? (size_t)soa_slots(s->clusterCount * kClusterSize) * sizeof(DevTri) : 0;
+    const size_t pfLds = (size_t)s->triPadded * sizeof(DevPrimF);
+    P.chainPrimF = s->chunkCount <= 1 && kChainStaticLds + recLds + pfLds <= kCuLds / (size_t)wgsPerCu;
+    const size_t floorLds = chain_lds_floor(wgsPerCu);
+    const size_t chainDyn = std::max<size_t>(recLds + (P.chainPrimF ? pfLds : 0),
+                                             floorLds > kChainStaticLds ? floorLds - kChainStaticLds : 0);
+    const dim3 grid(pl.gridX, pl.gridY);
+    const hipStream_t streams[rtcplan::kStreams] = {st, s->cst, ms->cst2, s->side};
+    const auto event = [&](int e) -> hipEvent_t {
+        if (e >= rtcplan::kEvSkyDone0 && e < rtcplan::kEvSkyDone0 + kSkySlots)
+            return s->evSkyDone[e - rtcplan::kEvSkyDone0];
+        if (e >= rtcplan::kEvGeoDone0 && e < rtcplan::kEvGeoDone0 + kSkySlots)
+            return s->evGeoDone[e - rtcplan::kEvGeoDone0];
+        switch (e) {
+        case rtcplan::kEvCullSync: return s->evCullSync;
+        case rtcplan::kEvFork: return s->evFork;
+        case rtcplan::kEvJoin: return s->evJoin;
+        case rtcplan::kEvFrame: return frameEvent;
+        case rtcplan::kEvGeometry: return geoEvent;
+        default: return nullptr;
+        }
+    };
+    for (int i = 0; i < pl.nOps; ++i) {
+        const rtcplan::Op &op = pl.ops[i];
+        const hipStream_t os = streams[op.stream];
+        const hipEvent_t ev = event(op.event);
+        if (op.kind == rtcplan::kOpRecord) {
+            if (ev) /* (the caller's hooks may be unarmed) */
+                HIP_TRY(hipEventRecord(ev, os));
+            continue;
+        }
+        if (op.kind == rtcplan::kOpWait) {
+            HIP_TRY(hipStreamWaitEvent(os, ev, 0));
+            continue;
+        }
+        switch (op.kernel) {
+        case rtcplan::kKPrep:
+            hipLaunchKernelGGL(rtc_prep_primary, dim3((s->triPadded + 8 + 63) / 64), dim3(64), 0, os, s->tris,
+                               const_cast<DevPrimF *>(P.primF), const_cast<DevPrimX *>(P.primX),
+                               s->triPadded > 0 ? s->triPadded + 8 : 0, P.origin, pl.prepCounts ? P.geoCount : nullptr);
+            HIP_TRY(hipGetLastError());
+            break;
+        case rtcplan::kKSuperCull:
+            hipLaunchKernelGGL(rtc_super_cull, dim3(pl.superX, pl.superY), dim3(64), 0, os, P, superMask);
+            HIP_TRY(hipGetLastError());
+            break;
+        case rtcplan::kKTileCull:
+            HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), os, ev,
+                                P, mask, weight, tileW, pixMask));
+            break;
+        case rtcplan::kKSky: {
             if (s->timing)
-                HIP_TRY(hipEventRecord(s->evSky0, skyStream));
-            const bool skyWide = smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
+                HIP_TRY(hipEventRecord(s->evSky0, os));
+            const bool skyWide = pl.smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
             if (skyWide)
-                hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0,
-                                   skyStream, P, (const unsigned *)tileW);
+                hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0, os,
+                                   P, (const unsigned *)tileW);
             else
-                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, skyStream, P,
+                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, os, P,
                                    (const unsigned *)tileW);
             HIP_TRY(hipGetLastError());
             if (s->timing)
-                HIP_TRY(hipEventRecord(s->evSky1, skyStream));
-            HIP_TRY(hipEventRecord(s->evJoin, s->side));
-            if (overlap) { /* this sky pass reads scratch slot `half` until evSkyDone[half] (recorded below) */
-                ms->skyPending[half] = true;
-                ms->skyKey[half] = key;
-                ms->skySeq[half] = ++ms->skyCount;
-            }
+                HIP_TRY(hipEventRecord(s->evSky1, os));
+            break;
+        }
+        case rtcplan::kKChain: {
             if (s->timing)
-                HIP_TRY(hipEventRecord(s->evHeavy0, gs));
-            /* dynamic LDS of the geometry kernel: the clustered records (single-chunk scenes), then the primary
-             * filter records when the block stays within 4 per CU */
-            const int wgsPerCu = smallShare ? RTC_CHAIN_WGS_SHARE : s->chainWgsFull;
-            const size_t rec = s->chunkCount <= 1 ? (size_t)soa_slots(s->clusterCount * kClusterSize) * sizeof(DevTri) : 0;
-            const size_t pf = (size_t)s->triPadded * sizeof(DevPrimF);
-            P.chainPrimF = s->chunkCount <= 1 && kChainStaticLds + rec + pf <= kCuLds / (size_t)wgsPerCu;
-            const size_t floorLds = chain_lds_floor(wgsPerCu);
-            const size_t dyn = std::max<size_t>(rec + (P.chainPrimF ? pf : 0),
-                                                floorLds > kChainStaticLds ? floorLds - kChainStaticLds : 0);
-            /* RTC_F_OVERLAP: evGeoDone (the frame event's order after the geometry pixels) is the completion of the
-             * launch stream's last kernel: the in-order sums, or the geometry kernel when it sums in-kernel */
-            hipEvent_t chainStop = overlap && (P.sampleCap == 0 || kAbNoSlots) ? s->evGeoDone[half] : nullptr;
+                HIP_TRY(hipEventRecord(s->evHeavy0, os));
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             if (s->chunkCount > 1 && dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, dyn, gs, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, chainDyn, os, ev, P));
             else if (s->chunkCount > 1)
-                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, dyn, gs, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, chainDyn, os, ev, P));
             else if (dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, dyn, gs, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, chainDyn, os, ev, P));
             else
-                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, dyn, gs, chainStop, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, chainDyn, os, ev, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
-                HIP_TRY(hipEventRecord(s->evHeavy1, gs));
-            if (P.sampleCap > 0 && !kAbNoSlots) {
-                const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
-                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, gs, overlap ? s->evGeoDone[half] : nullptr,
-                                    P));
-                HIP_TRY(hipGetLastError());
-            }
-            if (geoEvent) { /* the geometry pixels are done; the sky pass may still run */
-                HIP_TRY(hipEventRecord(geoEvent, gs));
-                geoRecorded = true;
-            }
-            ms->timed = s->timing;
-            if (overlap) {
-                /* no join: the frame is complete once the side stream has passed both passes (evGeoDone: recorded
-                 * by the last kernel above).  evSkyDone[half] marks that point too, so a later launch that waits for
-                 * this one (a conflicting buffer, the slot's reuse, a joined launch) waits for its geometry kernel as
-                 * well, wherever that ran (on the cull streams it is not ordered before the side stream's
-                 * sky pass).  `st` is not made to wait: with the geometry kernel on a cull stream the next launch's
-                 * cull stream waits for `st`'s position, which would order that geometry kernel after this one */
-                HIP_TRY(hipStreamWaitEvent(s->side, s->evGeoDone[half], 0));
-                HIP_TRY(hipEventRecord(s->evSkyDone[half], s->side));
-                if (frameEvent)
-                    HIP_TRY(hipEventRecord(frameEvent, s->side));
-                ms->slotUsed[half] = true;
-                ms->flip = (ms->flip + 1) % kSkySlots;
-                return 0;
-            }
-            HIP_TRY(hipStreamWaitEvent(st, s->evJoin, 0));
-            return finish();
+                HIP_TRY(hipEventRecord(s->evHeavy1, os));
+            break;
         }
-        ms->timed = false;
-        hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, st, weight, (int)blocks, order);
-        P.order = (d->flags & RTC_F_NO_REORDER) ? nullptr : order;
+        case rtcplan::kKAccum:
+            if (!kAbNoSlots) {
+                const unsigned g = (unsigned)std::min<size_t>(((size_t)P.sampleCap + 255) / 256, 1024);
+                HIP_TRY(launch_stop(rtc_accumulate_samples, dim3(g), dim3(256), 0, os, ev, P));
+            } else if (ev) {
+                HIP_TRY(hipEventRecord(ev, os));
+            }
+            break;
+        case rtcplan::kKOrder:
+            hipLaunchKernelGGL(rtc_order_blocks, dim3(1), dim3(1024), 0, os, weight, (int)pl.blocks, order);
+            HIP_TRY(hipGetLastError());
+            break;
+        case rtcplan::kKRender:
+            if (P.sphereCount > 0 && pl.debug)
+                hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, os, P);
+            else if (P.sphereCount > 0)
+                hipLaunchKernelGGL((rtc_render_kernel<true, false>), grid, dim3(kBlock), 0, os, P);
+            else if (pl.debug)
+                hipLaunchKernelGGL((rtc_render_kernel<false, true>), grid, dim3(kBlock), 0, os, P);
+            else
+                hipLaunchKernelGGL((rtc_render_kernel<false, false>), grid, dim3(kBlock), 0, os, P);
+            HIP_TRY(hipGetLastError());
+            break;
+        case rtcplan::kKReduce:
+            hipLaunchKernelGGL(rtc_reduce_segments, dim3(1), dim3(kSegSlots), 0, os, s->segSlots, dSegments);
+            HIP_TRY(hipGetLastError());
+            break;
+        default:
+            return rtc_fail(RTC_EINVAL, "rtc_render_rows_async: unknown planned kernel %d", op.kernel);
+        }
     }
-    if (P.sphereCount > 0 && debug)
-        hipLaunchKernelGGL((rtc_render_kernel<true, true>), grid, dim3(kBlock), 0, st, P);
-    else if (P.sphereCount > 0)
-        hipLaunchKernelGGL((rtc_render_kernel<true, false>), grid, dim3(kBlock), 0, st, P);
-    else if (debug)
-        hipLaunchKernelGGL((rtc_render_kernel<false, true>), grid, dim3(kBlock), 0, st, P);
-    else
-        hipLaunchKernelGGL((rtc_render_kernel<false, false>), grid, dim3(kBlock), 0, st, P);
-    HIP_TRY(hipGetLastError());
-    return finish();
+    ms->timed = pl.fused && s->timing;
+    ms->plan = pl.after; /* every operation is enqueued */
+    return 0;
 }
 
 /* ---- row de-interleave after a gather (bytes) ----------------------------------------------------- */
