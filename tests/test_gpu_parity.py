@@ -666,7 +666,6 @@ def test_render_multi_rccl_equals_render(name, band, gpu_available):
     assert np.array_equal(a, b) and np.array_equal(_bits(fa), _bits(fb))
     assert sa["segments"] == sb["segments"]
     assert 0 < sb["render_ms"] <= sb["frame_ms"] <= sb["total_ms"]
-    assert rt.last_multi_info() == {"path": "host_rows", "devices": rt.device_count(), "comm_ranks": []}
     assert 0 < sa["render_ms"] <= sa["frame_ms"] <= sa["total_ms"]
     # every communicator of the clique reports the whole clique (ncclCommCount)
     info = rt.last_multi_info()
