@@ -1395,12 +1395,6 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
-#ifndef RTC_CULL_READLANE
-#define RTC_CULL_READLANE 1 /* (A/B switch, round 6) */
-#endif
-#ifndef RTC_XCD_ITEMS
-#define RTC_XCD_ITEMS 1 /* (A/B switch, round 6) */
-#endif
 constexpr int kChainBlock = 256; /* threads per chain workgroup (two-wave workgroups were slower everywhere, r04_ze) */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
@@ -1568,8 +1562,6 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
     const bool table = !MULTI && firstBounce && P.clusterCull && !__ballot(alive && !rhoOk);
     unsigned long long reach[kChunkClusters * kClusterSize / 64];
     unsigned long long live = 0; /* clusters with a record reachable from p0 (their terms compacted in W.cl) */
-    ClusterTerms myT{V3{0.f, 0.f, 0.f}, 0.f, 0.f, 0.f}; /* lane k: cluster k's origin terms (RTC_CULL_READLANE) */
-    unsigned myR8 = 0;
     DSECT_BEGIN(dtab);
     if (table) {
         const V3 p0{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pos.x), 0)),
@@ -1603,11 +1595,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)live, 0u));
             /* (the workgroup's LDS copy of the clusters: a global load here was a round trip on every window) */
             const ClusterTerms t = cluster_terms(p0, sCl[lane]);
-            if (!RTC_CULL_READLANE)
-                W.cl[pos][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
+            W.cl[pos][0] = make_float4(t.w.x, t.w.y, t.w.z, t.w2);
             W.cl[pos][1] = make_float4(t.A, t.B, __int_as_float(lane), __int_as_float((int)r8l));
-            myT = t;
-            myR8 = r8l;
         }
         wave_lds_sync();
     }
@@ -1671,20 +1660,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         /* table mode: bit j of cm = the j-th live cluster kept (branch-free body over the compacted terms) */
         const int nLive = __popcll(live);
         if (dense) {
-        } else if (in && table && RTC_CULL_READLANE) {
-            /* the live clusters' terms from the lanes that computed them (v_readlane: no LDS round trip per group of
-             * clusters); bit j of cm = the j-th live cluster, the W.cl order the pair passes use */
-            unsigned long long lv = live;
-            for (int j = 0; lv; ++j, lv &= lv - 1) {
-                const int k = __builtin_ctzll(lv);
-                const auto rl = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); };
-                const ClusterTerms t{V3{rl(myT.w.x), rl(myT.w.y), rl(myT.w.z)}, rl(myT.w2), rl(myT.A), rl(myT.B)};
-                const bool kept = !(rhoOk && culled_by(t, dir, rho, dd));
-                cm |= (unsigned)kept << j;
-                if (COUNT)
-                    tests += kept ? (unsigned)__popc((unsigned)__builtin_amdgcn_readlane((int)myR8, k)) : 0u;
-            }
         } else if (in && table) {
+            /* (round 6: each live cluster's terms by v_readlane from the lane that computed them instead of these LDS
+             * reads -- six VALU readlanes per cluster: chain kernel +3 %, frame +2.4 %, profiles/r06_c_ab_*) */
 #pragma unroll 4
             for (int j = 0; j < nLive; ++j) {
                 const float4 a = W.cl[j][0], b = W.cl[j][1];
@@ -1907,6 +1885,13 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * shortened the kernel 4 % but made every workgroup retire at its end, so the sky pass no longer filled the
      * tail: frame 0.396 -> 0.42 ms). */
     int nextIt = 0;
+    /* (Global item counters instead, round 5: the kernel 6 % shorter, the frame 3-4 % longer -- the sky pass no longer
+     * fills its tail -- and small shares 17-28 % longer.  Items grouped by XCD, round 6 -- XCD group b % 8 taking the
+     * (b % 8)-th eighth of the list, so that a tile's neighbouring pixels share an L2: frame 0.333 -> 0.358 ms, 1/8 share
+     * 0.068 -> 0.079 ms, profiles/r06_c_ab_xcd_items_readlane_cull.log.) */
+    const auto next_item = [&]() { return (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x; };
+    if (lane == 0)
+        nextIt = next_item();
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
      * segment where they are used: KARG) */
 #ifdef RTC_DIAG_COUNT /* diagnostic variant: the test counters on in every launch (rtc_diag_itemlog's tests) */
@@ -1929,28 +1914,6 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             incl += v;
     }
     const int nItems = __builtin_amdgcn_readlane(incl, kGeoLists - 1);
-    /* The items by XCD (round 6): blocks b and b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md; a speed
-     * label only), so XCD group g = b % 8 takes the g-th eighth of the concatenated item list, and block b its items
-     * b / 8 + k * (grid / 8) of that range.  A tile's geometry pixels are consecutive items: they now land on one XCD, so
-     * its mask words and list entries are read through one L2, and the 3-byte Color stores of neighbouring pixels
-     * merge in that L2 instead of being written back partially by up to eight.  Within a block the
-     * waves still take the next k from the LDS counter.  (Global item counters instead, round 5: the kernel 6 % shorter,
-     * the frame 3-4 % longer -- the sky pass no longer fills its tail -- and small shares 17-28 % longer.) */
-#if RTC_XCD_ITEMS
-    const int nGrp = (gridDim.x & 7u) == 0 ? 8 : 1;
-#else
-    const int nGrp = 1;
-#endif
-    const int grpChunk = (nItems + nGrp - 1) / nGrp;
-    const int grpLo = min(nItems, ((int)blockIdx.x % nGrp) * grpChunk);
-    const int grpCnt = min(nItems, grpLo + grpChunk) - grpLo;
-    const int grpBlock = (int)blockIdx.x / nGrp, grpBlocks = (int)gridDim.x / nGrp;
-    const auto next_item = [&]() {
-        const int q = grpBlock + atomicAdd(&sWork, 1) * grpBlocks;
-        return q < grpCnt ? grpLo + q : nItems;
-    };
-    if (lane == 0)
-        nextIt = next_item();
     /* Prefetch (round 5): an item's list entry and its tile's first two mask words were written by the tile cull on
      * other XCDs, so their first reads miss this XCD's L2; read as scalar loads at the item's start they were a chain
      * of dependent misses on the critical path of every item (round-4 stamps: item setup 17 % of the waves' lifetime).
