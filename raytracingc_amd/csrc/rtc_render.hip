@@ -1395,6 +1395,12 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
+#ifndef RTC_ITEM_STRIDED
+#define RTC_ITEM_STRIDED 1 /* (A/B switch, round 6) */
+#endif
+#ifndef RTC_EARLY_COUNTS
+#define RTC_EARLY_COUNTS 1 /* (A/B switch, round 6) */
+#endif
 constexpr int kChainBlock = 256; /* threads per chain workgroup (two-wave workgroups were slower everywhere, r04_ze) */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
  * so that a quarter of every SIMD's registers holds two sky waves (<= 64 VGPRs) from the start: the sky pass then runs
@@ -1748,9 +1754,13 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 {
     int items = 0;
     for (int l = 0; l < kGeoLists; ++l)
-        items += min(P.geoCount[l * kGeoCountStride], P.geoCap);
+        items = RTC_ITEM_STRIDED ? max(items, kGeoLists * min(P.geoCount[l * kGeoCountStride], P.geoCap))
+                                 : items + min(P.geoCount[l * kGeoCountStride], P.geoCap);
     items = min(items, P.sampleCap);
     for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
+        /* (strided items: item it is entry it / kGeoLists of sub-list it % kGeoLists, if that sub-list holds it) */
+        if (RTC_ITEM_STRIDED && it / kGeoLists >= min(P.geoCount[(it % kGeoLists) * kGeoCountStride], P.geoCap))
+            continue;
         const SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
         f2 accxy{0.f, 0.f};
         float accz = 0.f;
@@ -1858,10 +1868,24 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
     __shared__ DevCluster sCl[kChunkClusters]; /* single-chunk scenes: the clusters, for the dense culls */
+#if RTC_EARLY_COUNTS
+    /* the sub-list counts first (written by the tile cull, likely on another XCD: a miss in this one's L2), so that their
+     * round trip overlaps the staging below instead of following it on the way to the first item */
+    const int count0 = (threadIdx.x & 63) < kGeoLists ? (int)gload(P.geoCount, (size_t)(threadIdx.x & 63) * kGeoCountStride) : 0;
+#endif
+#if RTC_ITEM_STRIDED
+    /* items strided over the sub-lists (item i: entry i / kGeoLists of sub-list i % kGeoLists, valid when that sub-list
+     * holds it), so an item's entry address needs no counts: each wave's first item (b + w * grid, handed out statically)
+     * is requested here, before the staging, and arrives with the counts */
+    const int it0 = (int)blockIdx.x + (int)(threadIdx.x >> 6) * (int)gridDim.x;
+    const unsigned vc0 = (it0 / kGeoLists) < P.geoCap
+                             ? gload(P.geoList, (size_t)(it0 % kGeoLists) * P.geoCap + (size_t)(it0 / kGeoLists) + vzero())
+                             : 0u;
+#endif
     if (!MULTI && threadIdx.x < P.clusterCount && threadIdx.x < kChunkClusters)
         sCl[threadIdx.x] = P.clusters[threadIdx.x];
     if (threadIdx.x == 0)
-        sWork = 0;
+        sWork = RTC_ITEM_STRIDED ? kChainBlock / 64 : 0; /* (strided: k = 0 .. waves - 1 went to the waves statically) */
     sPow.fill(threadIdx.x);
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
     const float4 *sRec = S.rec;
@@ -1889,9 +1913,11 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * fills its tail -- and small shares 17-28 % longer.  Items grouped by XCD, round 6 -- XCD group b % 8 taking the
      * (b % 8)-th eighth of the list, so that a tile's neighbouring pixels share an L2: frame 0.333 -> 0.358 ms, 1/8 share
      * 0.068 -> 0.079 ms, profiles/r06_c_ab_xcd_items_readlane_cull.log.) */
+#if !RTC_ITEM_STRIDED
     const auto next_item = [&]() { return (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x; };
     if (lane == 0)
         nextIt = next_item();
+#endif
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
      * segment where they are used: KARG) */
 #ifdef RTC_DIAG_COUNT /* diagnostic variant: the test counters on in every launch (rtc_diag_itemlog's tests) */
@@ -1906,7 +1932,30 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     /* the sub-lists' inclusive prefix counts, lane l < kGeoLists holding sub-list l's, loaded once per wave: an
      * item's sub-list is then a ballot, not a chain of dependent count loads as a wave's items pass the sub-lists */
+#if RTC_ITEM_STRIDED
+    const int cnt = lane < kGeoLists ? min(count0, P.geoCap) : 0; /* sub-list `lane`'s entries */
+    int mx = cnt;
+#pragma unroll
+    for (int d = 1; d < kGeoLists; d <<= 1)
+        mx = max(mx, __shfl_xor(mx, d));
+    const int nItems = kGeoLists * __builtin_amdgcn_readfirstlane(mx); /* (items past a sub-list's count are skipped) */
+    const auto valid = [&](int i) { return i / kGeoLists < __builtin_amdgcn_readlane(cnt, i % kGeoLists); };
+    const auto next_item = [&]() {
+        int q;
+        do
+            q = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
+        while (q < nItems && !valid(q));
+        return q;
+    };
+    const auto entry_of = [&](int it2) -> size_t {
+        return (size_t)(it2 % kGeoLists) * KARG(geoCap) + (size_t)(it2 / kGeoLists);
+    };
+#else
+#if RTC_EARLY_COUNTS
+    int incl = lane < kGeoLists ? min(count0, P.geoCap) : 0;
+#else
     int incl = lane < kGeoLists ? min(P.geoCount[lane * kGeoCountStride], P.geoCap) : 0;
+#endif
 #pragma unroll
     for (int d = 1; d < kGeoLists; d <<= 1) {
         const int v = __shfl_up(incl, d);
@@ -1927,16 +1976,32 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
         return (size_t)l * KARG(geoCap) + (size_t)(it2 - base);
     };
+#endif
     const auto mask_dwords = [&](int code2) -> unsigned {
         const unsigned *mw = (const unsigned *)(KARG(tileMask) + (size_t)(code2 >> 6) * P.maskWords);
         return lane < 2 * P.maskWords && lane < 4 ? gload(mw, (size_t)lane) : 0u;
     };
-    int it = __builtin_amdgcn_readfirstlane(nextIt);
     unsigned vc = 0, vm = 0; /* the current item's entry and mask dwords (vector registers) */
+#if RTC_ITEM_STRIDED
+    int it = it0;
+    if (it < nItems && valid(it)) {
+        vc = vc0;
+    } else {
+        if (lane == 0)
+            nextIt = next_item();
+        it = __builtin_amdgcn_readfirstlane(nextIt);
+        if (it < nItems)
+            vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
+    }
+    if (it < nItems)
+        vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
+#else
+    int it = __builtin_amdgcn_readfirstlane(nextIt);
     if (it < nItems) {
         vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
         vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
     }
+#endif
     if (lane == 0)
         nextIt = next_item();
     DMARK(dcur, 19); /* prologue: staging, tables, the first item */

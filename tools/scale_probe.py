@@ -19,7 +19,8 @@ from conftest import load_tris  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 W, H, SPP = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 kernel = sys.argv[5] if len(sys.argv) > 5 else "chain"
-extra = {"chain": {}, "overlap": {"overlap": True}, "overlap_inline": {"overlap": True, "chain_inline": True}}[kernel]
+extra = {"chain": {}, "overlap": {"overlap": True}, "overlap_inline": {"overlap": True, "chain_inline": True},
+         "overlap_hoist": {"overlap": True, "hoist": True}}[kernel]
 NS = tuple(int(v) for v in os.environ.get("SCALE_NS", "1,2,4,8").split(","))
 BAND = int(os.environ.get("SCALE_BAND", "1"))  # rows per interleaved band (rtc.h rowBand; 1: single rows)
 tris, _ = load_tris("ultracomplex")
