@@ -74,6 +74,11 @@ void plan_launch(const State &s, const Request &r, Plan &p)
      * (DESIGN §3); smaller whole frames keep the caller's stream (C1 256x256x1: cross-stream hops would be its period) */
     p.smallShare = r.rowStride > 1 && px <= kInlineSumPixels;
     p.chainOnCs = p.overlap && (p.smallShare || px > kInlineSumPixels);
+    /* Round 6: a pipelined launch on the alternating streams runs its sky pass AFTER its geometry kernel
+     * (which then writes each pixel's colour into a per-item word, not into Color) and the sky pass writes every pixel of
+     * the frame in whole 64-B lines -- no partial line written back from up to eight XCDs' L2s.  In the pipelined steady
+     * state this sky pass runs beside the next frame's geometry kernel, as the previous one did beside this frame's. */
+    p.merge = p.chainOnCs && !r.noMerge;
     p.needCst2 = p.chainOnCs && !s.cst2;
     if (p.needCst2)
         n.cst2 = true;
@@ -106,7 +111,8 @@ void plan_launch(const State &s, const Request &r, Plan &p)
      * launches of different sizes are in flight together (round 5 fix; the legacy layout is a test hook) */
     if (p.cull) {
         const size_t need = maskBytes + p.tiles * 8 + (p.blocks + p.tiles + p.blocks + 4) * 4 +
-                            ((size_t)kGeoLists * kGeoCountStride + (size_t)kGeoLists * p.geoCap) * 4 + 8 + superBytes;
+                            ((size_t)kGeoLists * kGeoCountStride + (size_t)kGeoLists * p.geoCap) * 4 + 8 + superBytes +
+                            256 + p.tiles * 64 * 4 + (size_t)kGeoLists * p.geoCap * 4; /* + pixItem, geoColor */
         p.slotBytes = align_up(need, 256);
         p.scratchNeed = kSlots * p.slotBytes;
         p.scratchGrow = p.scratchNeed > s.scratchCap;
@@ -122,7 +128,9 @@ void plan_launch(const State &s, const Request &r, Plan &p)
         L.order = L.tileW + p.tiles * 4;
         L.geoList = L.order + (p.blocks + 4 + (size_t)kGeoLists * kGeoCountStride) * 4;
         L.superMask = align_up(L.geoList + (size_t)kGeoLists * p.geoCap * 4, 8);
-        L.end = L.superMask + superBytes;
+        L.pixItem = align_up(L.superMask + superBytes, 256);
+        L.geoColor = L.pixItem + p.tiles * 64 * 4;
+        L.end = L.geoColor + (size_t)kGeoLists * p.geoCap * 4;
     }
     if (p.chain) {
         p.geoSet = s.geoSeq % kGeoRing;
@@ -190,7 +198,21 @@ void plan_launch(const State &s, const Request &r, Plan &p)
             E.kernel(kStCaller, kKOrder);
             E.kernel(kStCaller, kKRender);
         } else {
-            /* the sky pixels on the side stream, concurrently with the geometry kernel */
+            /* the sky pixels on the side stream: concurrently with the geometry kernel, or (merge) after it */
+            if (p.merge) {
+                E.kernel(p.gs, kKChain, kEvGeoDone0 + p.half);
+                E.record(p.gs, kEvGeometry);
+                E.wait(kStSide, kEvGeoDone0 + p.half); /* (after the cull too: the geometry kernel follows it on gs) */
+                E.kernel(kStSide, kKSky);
+                n.skyPending[p.half] = true;
+                n.skyKey[p.half] = r.key;
+                n.skySeq[p.half] = ++n.skyCount;
+                E.record(kStSide, kEvSkyDone0 + p.half);
+                E.record(kStSide, kEvFrame);
+                n.slotUsed[p.half] = true;
+                n.flip = (s.flip + 1) % kSlots;
+                return;
+            }
             E.wait(kStSide, kEvFork);
             E.kernel(kStSide, kKSky);
             E.record(kStSide, kEvJoin);
@@ -263,12 +285,18 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         scratch(kWrite, L.mask, L.order); /* mask, pixMask, weight, tileW */
         if (p.chain) {
             scratch(kWrite, L.geoList, L.superMask);
+            if (p.merge)
+                scratch(kWrite, L.pixItem, L.geoColor);
             put(kResGeoSet, kAtomic, p.geoSet, 0, 1);
             put(kResGeoSet, kWrite, p.geoSetNext, 0, 1);
         }
         break;
     case kKSky:
         scratch(kRead, L.pixMask, L.order);
+        if (p.merge) {
+            scratch(kRead, L.pixItem, L.geoColor);
+            scratch(kRead, L.geoColor, L.end);
+        }
         colors();
         if (r.segments)
             put(kResSegSlots, kAtomic, 0, 0, 1);
@@ -280,7 +308,13 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         put(kResGeoSet, kRead, p.geoSet, 0, 1);
         if (p.sampleCap > 0)
             put(kResSamples, kWrite, 0, 0, 1);
-        colors();
+        if (p.merge) {
+            scratch(kWrite, L.geoColor, L.end);
+            if (r.key.accum)
+                put(kResAccum, kKeyedWrite, r.key.accum, 0, 1);
+        } else {
+            colors();
+        }
         if (r.segments)
             put(kResSegSlots, kAtomic, 0, 0, 1);
         break;

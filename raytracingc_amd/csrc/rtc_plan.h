@@ -89,16 +89,21 @@ struct Request {
     Key key;
     float origin[3];
     bool legacySlotLayout; /* test hook: round 5's broken layout (slot h at h x this launch's slot size) */
+    bool noMerge;          /* the sky pass beside the geometry kernel even where it could follow it (A/B) */
 };
 
 /* byte offsets inside one scratch slot (the tile cull's outputs, rtc_render.hip) */
 struct Layout {
-    size_t mask, pixMask, weight, tileW, order, geoList, superMask, end;
+    size_t mask, pixMask, weight, tileW, order, geoList, superMask;
+    size_t pixItem;  /* per pixel (tile * 64 + bit) of the geometry pixels: its item (merged sky pass) */
+    size_t geoColor; /* per item: its Color bytes (merged sky pass) */
+    size_t end;
 };
 
 struct Plan {
     bool empty;          /* no rows: only the caller's hooks are recorded */
     bool cull, fused, chain, overlap, smallShare, chainOnCs, superCull, debug;
+    bool merge;          /* the sky pass follows the geometry kernel and writes every pixel's Color in whole lines */
     int half;            /* the scratch slot */
     int cs, gs;          /* the culls' stream and the geometry kernel's (Stream) */
     unsigned gridX, gridY, superX, superY;

@@ -125,6 +125,11 @@ struct RenderParams {
     int geoCap; /* entries per sub-list */
     int cullPrio; /* rtc_tile_cull's waves at issue priority 3 (kCullPrioMinPixels) */
     int blocksX; /* 16x16 blocks per row of the launch */
+    /* merged sky pass (rtcplan::Plan::merge; null: none): rtc_tile_cull writes each geometry pixel's item (pixItem[tile * 64
+     * + bit]), rtc_render_chain each item's Color bytes (geoColor[item], bytes 0-2), and the sky pass -- after it -- every
+     * pixel's Color in whole lines */
+    unsigned *__restrict__ pixItem;
+    unsigned *__restrict__ geoColor;
     SampleSlot *__restrict__ sampleBuf; /* rtc_render_chain, deferred accumulation: [item][spp] radiance * (1/spp) */
     int *__restrict__ itemPix;      /* [item] the pixel's offset in the launch's Color rows */
     int sampleCap;                  /* items with a slot in sampleBuf; items beyond it accumulate in-kernel */
@@ -972,8 +977,12 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
             base = __builtin_amdgcn_readfirstlane(base);
             /* a sub-list holds every geometry pixel of its tiles (geoCap = 64 x its tiles) when its counter started at
              * 0; a stale counter must not write past it (the readers clamp the counts to geoCap too) */
-            if (((gb >> lane) & 1ull) && base + __popcll(gb) <= P.geoCap)
-                P.geoList[(size_t)l * P.geoCap + base + __popcll(gb & ((1ull << lane) - 1ull))] = tile * 64 + lane;
+            if (((gb >> lane) & 1ull) && base + __popcll(gb) <= P.geoCap) {
+                const int pos = base + __popcll(gb & ((1ull << lane) - 1ull));
+                P.geoList[(size_t)l * P.geoCap + pos] = tile * 64 + lane;
+                if (P.pixItem) /* the pixel's entry: pos of sub-list l (the sky pass turns it into its item) */
+                    P.pixItem[(size_t)tile * 64 + lane] = (unsigned)(pos * kGeoLists + l);
+            }
         };
         append(b, tile % kGeoLists);
     }
@@ -1313,16 +1322,39 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
     unsigned segCalls = 0, segTraced = 0;
     const int r = (int)blockIdx.y * kSkyWaves + __builtin_amdgcn_readfirstlane(lw); /* launch row (wave-uniform) */
     const int x = (int)blockIdx.x * 64 + lane;
-    bool valid = r < P.rows && x < P.width;
+    const bool inFrame = r < P.rows && x < P.width;
     /* the pixel's tile: pixels with a primary candidate are rtc_render_chain's (pixMask bit (row % 8) * 8 + x % 8) */
-    if (valid) {
-        const int t = (r >> 3) * (P.blocksX * 2) + (x >> 3);
-        const bool geo = tileW[t] > 0 && ((P.pixMask[t] >> (((r & 7) << 3) | (x & 7))) & 1ull);
-        valid = !geo;
+    bool geo = false;
+    int t = 0;
+    if (inFrame) {
+        t = (r >> 3) * (P.blocksX * 2) + (x >> 3);
+        geo = tileW[t] > 0 && ((P.pixMask[t] >> (((r & 7) << 3) | (x & 7))) & 1ull);
     }
-    const unsigned long long mine = __ballot(valid);
+    const bool valid = inFrame && !geo; /* a sky pixel: this kernel renders it */
+    /* merged (P.geoColor): the geometry kernel has finished; its pixels' bytes are written here too, so every strip is
+     * whole lines.  Their words are requested now and used after the sky loop. */
+    const bool merged = P.geoColor != nullptr; /* (uniform) */
+    const bool writes = merged ? inFrame : valid;
+    const unsigned long long mine = __ballot(writes);
     if (mine == 0ull)
         return;
+    unsigned gw = 0;
+    if (merged) {
+        /* the geometry kernel's items are the sub-lists concatenated: entry pos of sub-list l is item (entries of the
+         * sub-lists before l) + pos -- the exclusive prefix of the launch's counts, lane l holding sub-list l's */
+        const int cnt = lane < kGeoLists ? min(P.geoCount[lane * kGeoCountStride], P.geoCap) : 0;
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < kGeoLists; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d)
+                incl += v;
+        }
+        const unsigned e = geo ? P.pixItem[(size_t)t * 64 + (((r & 7) << 3) | (x & 7))] : 0u;
+        const int excl = __shfl(incl - cnt, (int)(e % kGeoLists));
+        if (geo)
+            gw = P.geoColor[excl + (int)(e / kGeoLists)];
+    }
     const int y = launch_row_y(P, r);
     const V3 dir = primary_dir(P, x, y);
     V3 acc{0.f, 0.f, 0.f};
@@ -1348,8 +1380,10 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
         segCalls = (unsigned)P.spp;
         segTraced = P.hoist ? 1u : (unsigned)P.spp;
     }
-    /* vec3ToColor (raytracing.c:11-15, main.c:101) */
-    const unsigned char c0 = float_to_u8(acc.x), c1 = float_to_u8(acc.y), c2 = float_to_u8(acc.z);
+    /* vec3ToColor (raytracing.c:11-15, main.c:101); a geometry pixel's bytes as the geometry kernel quantised them */
+    const unsigned char c0 = valid ? float_to_u8(acc.x) : (unsigned char)(gw & 0xffu);
+    const unsigned char c1 = valid ? float_to_u8(acc.y) : (unsigned char)((gw >> 8) & 0xffu);
+    const unsigned char c2 = valid ? float_to_u8(acc.z) : (unsigned char)((gw >> 16) & 0xffu);
     unsigned char *const rowp = P.colors + 3 * ((size_t)r * (size_t)P.width + (size_t)blockIdx.x * 64);
     const bool whole = mine == ~0ull && ((uintptr_t)rowp & 15u) == 0u; /* wave-uniform */
     if (whole) {
@@ -1360,7 +1394,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
         wave_lds_sync();
         if (lane < 12)
             ((uint4 *)rowp)[lane] = ((const uint4 *)st)[lane];
-    } else if (valid) {
+    } else if (writes) {
         rowp[3 * lane] = c0;
         rowp[3 * lane + 1] = c1;
         rowp[3 * lane + 2] = c2;
@@ -1395,11 +1429,8 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
-#ifndef RTC_ITEM_STRIDED
-#define RTC_ITEM_STRIDED 1 /* (A/B switch, round 6) */
-#endif
-#ifndef RTC_EARLY_COUNTS
-#define RTC_EARLY_COUNTS 1 /* (A/B switch, round 6) */
+#ifndef RTC_SKY_MERGE
+#define RTC_SKY_MERGE 1 /* (A/B switch, round 6) */
 #endif
 constexpr int kChainBlock = 256; /* threads per chain workgroup (two-wave workgroups were slower everywhere, r04_ze) */
 /* Persistent chain workgroups per CU (each 4 waves of 128 VGPRs: 4 fill every SIMD's registers).  A whole frame runs 3,
@@ -1754,13 +1785,9 @@ __global__ __launch_bounds__(256) void rtc_accumulate_samples(RenderParams P)
 {
     int items = 0;
     for (int l = 0; l < kGeoLists; ++l)
-        items = RTC_ITEM_STRIDED ? max(items, kGeoLists * min(P.geoCount[l * kGeoCountStride], P.geoCap))
-                                 : items + min(P.geoCount[l * kGeoCountStride], P.geoCap);
+        items += min(P.geoCount[l * kGeoCountStride], P.geoCap);
     items = min(items, P.sampleCap);
     for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
-        /* (strided items: item it is entry it / kGeoLists of sub-list it % kGeoLists, if that sub-list holds it) */
-        if (RTC_ITEM_STRIDED && it / kGeoLists >= min(P.geoCount[(it % kGeoLists) * kGeoCountStride], P.geoCap))
-            continue;
         const SampleSlot *slot = P.sampleBuf + (size_t)it * (size_t)P.spp;
         f2 accxy{0.f, 0.f};
         float accz = 0.f;
@@ -1868,24 +1895,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     __shared__ ChainWaveLds sWave[kChainBlock / 64];
     __shared__ int sWork; /* the workgroup's next item (see below) */
     __shared__ DevCluster sCl[kChunkClusters]; /* single-chunk scenes: the clusters, for the dense culls */
-#if RTC_EARLY_COUNTS
-    /* the sub-list counts first (written by the tile cull, likely on another XCD: a miss in this one's L2), so that their
-     * round trip overlaps the staging below instead of following it on the way to the first item */
-    const int count0 = (threadIdx.x & 63) < kGeoLists ? (int)gload(P.geoCount, (size_t)(threadIdx.x & 63) * kGeoCountStride) : 0;
-#endif
-#if RTC_ITEM_STRIDED
-    /* items strided over the sub-lists (item i: entry i / kGeoLists of sub-list i % kGeoLists, valid when that sub-list
-     * holds it), so an item's entry address needs no counts: each wave's first item (b + w * grid, handed out statically)
-     * is requested here, before the staging, and arrives with the counts */
-    const int it0 = (int)blockIdx.x + (int)(threadIdx.x >> 6) * (int)gridDim.x;
-    const unsigned vc0 = (it0 / kGeoLists) < P.geoCap
-                             ? gload(P.geoList, (size_t)(it0 % kGeoLists) * P.geoCap + (size_t)(it0 / kGeoLists) + vzero())
-                             : 0u;
-#endif
     if (!MULTI && threadIdx.x < P.clusterCount && threadIdx.x < kChunkClusters)
         sCl[threadIdx.x] = P.clusters[threadIdx.x];
     if (threadIdx.x == 0)
-        sWork = RTC_ITEM_STRIDED ? kChainBlock / 64 : 0; /* (strided: k = 0 .. waves - 1 went to the waves statically) */
+        sWork = 0;
     sPow.fill(threadIdx.x);
     const ChainStage S = chain_stage<MULTI>(P, sDyn);
     const float4 *sRec = S.rec;
@@ -1913,11 +1926,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * fills its tail -- and small shares 17-28 % longer.  Items grouped by XCD, round 6 -- XCD group b % 8 taking the
      * (b % 8)-th eighth of the list, so that a tile's neighbouring pixels share an L2: frame 0.333 -> 0.358 ms, 1/8 share
      * 0.068 -> 0.079 ms, profiles/r06_c_ab_xcd_items_readlane_cull.log.) */
-#if !RTC_ITEM_STRIDED
     const auto next_item = [&]() { return (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x; };
     if (lane == 0)
         nextIt = next_item();
-#endif
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg
      * segment where they are used: KARG) */
 #ifdef RTC_DIAG_COUNT /* diagnostic variant: the test counters on in every launch (rtc_diag_itemlog's tests) */
@@ -1932,30 +1943,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
 #endif
     /* the sub-lists' inclusive prefix counts, lane l < kGeoLists holding sub-list l's, loaded once per wave: an
      * item's sub-list is then a ballot, not a chain of dependent count loads as a wave's items pass the sub-lists */
-#if RTC_ITEM_STRIDED
-    const int cnt = lane < kGeoLists ? min(count0, P.geoCap) : 0; /* sub-list `lane`'s entries */
-    int mx = cnt;
-#pragma unroll
-    for (int d = 1; d < kGeoLists; d <<= 1)
-        mx = max(mx, __shfl_xor(mx, d));
-    const int nItems = kGeoLists * __builtin_amdgcn_readfirstlane(mx); /* (items past a sub-list's count are skipped) */
-    const auto valid = [&](int i) { return i / kGeoLists < __builtin_amdgcn_readlane(cnt, i % kGeoLists); };
-    const auto next_item = [&]() {
-        int q;
-        do
-            q = (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x;
-        while (q < nItems && !valid(q));
-        return q;
-    };
-    const auto entry_of = [&](int it2) -> size_t {
-        return (size_t)(it2 % kGeoLists) * KARG(geoCap) + (size_t)(it2 / kGeoLists);
-    };
-#else
-#if RTC_EARLY_COUNTS
-    int incl = lane < kGeoLists ? min(count0, P.geoCap) : 0;
-#else
     int incl = lane < kGeoLists ? min(P.geoCount[lane * kGeoCountStride], P.geoCap) : 0;
-#endif
 #pragma unroll
     for (int d = 1; d < kGeoLists; d <<= 1) {
         const int v = __shfl_up(incl, d);
@@ -1976,32 +1964,16 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         const int base = l ? __builtin_amdgcn_readlane(incl, l - 1) : 0;
         return (size_t)l * KARG(geoCap) + (size_t)(it2 - base);
     };
-#endif
     const auto mask_dwords = [&](int code2) -> unsigned {
         const unsigned *mw = (const unsigned *)(KARG(tileMask) + (size_t)(code2 >> 6) * P.maskWords);
         return lane < 2 * P.maskWords && lane < 4 ? gload(mw, (size_t)lane) : 0u;
     };
-    unsigned vc = 0, vm = 0; /* the current item's entry and mask dwords (vector registers) */
-#if RTC_ITEM_STRIDED
-    int it = it0;
-    if (it < nItems && valid(it)) {
-        vc = vc0;
-    } else {
-        if (lane == 0)
-            nextIt = next_item();
-        it = __builtin_amdgcn_readfirstlane(nextIt);
-        if (it < nItems)
-            vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
-    }
-    if (it < nItems)
-        vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
-#else
     int it = __builtin_amdgcn_readfirstlane(nextIt);
+    unsigned vc = 0, vm = 0; /* the current item's entry and mask dwords (vector registers) */
     if (it < nItems) {
         vc = gload(KARG(geoList), entry_of(it) + (size_t)vzero());
         vm = mask_dwords(__builtin_amdgcn_readfirstlane((int)vc));
     }
-#endif
     if (lane == 0)
         nextIt = next_item();
     DMARK(dcur, 19); /* prologue: staging, tables, the first item */
@@ -2288,6 +2260,15 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
         if (deferred) {
             if (lane == 0)
                 P.itemPix[it] = r * KARG(width) + x;
+        } else if (P.geoColor) { /* merged sky pass: the pixel's three bytes as one word of its item */
+            const unsigned b = float_to_u8(acc);
+            const unsigned w = (unsigned)__builtin_amdgcn_readlane((int)b, 0) |
+                               (unsigned)__builtin_amdgcn_readlane((int)b, 1) << 8 |
+                               (unsigned)__builtin_amdgcn_readlane((int)b, 2) << 16;
+            if (lane == 0)
+                P.geoColor[it] = w;
+            if (lane < 3 && P.accum)
+                P.accum[3 * ((size_t)r * (size_t)KARG(width) + (size_t)x) + (size_t)lane] = acc;
         } else if (lane < 3) {
             const size_t o = 3 * ((size_t)r * (size_t)KARG(width) + (size_t)x) + (size_t)lane;
             P.colors[o] = float_to_u8(acc);
@@ -2484,6 +2465,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     rq.segments = dSegments != nullptr;
     rq.key = sky_key(P);
     memcpy(rq.origin, &P.origin, sizeof rq.origin);
+    rq.noMerge = !RTC_SKY_MERGE;
     static thread_local rtcplan::Plan pl;
     rtcplan::plan_launch(s->plan, rq, pl);
     /* the saved state claims only what has been enqueued: until every operation below is, a later launch sees none of
@@ -2527,6 +2509,10 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
         tileW = (unsigned *)(slot + pl.lay.tileW);
         order = (int *)(slot + pl.lay.order);
         superMask = (unsigned long long *)(slot + pl.lay.superMask);
+        if (pl.merge) {
+            P.pixItem = (unsigned *)(slot + pl.lay.pixItem);
+            P.geoColor = (unsigned *)(slot + pl.lay.geoColor);
+        }
         P.tileMask = mask;
         P.pixMask = pixMask;
         if (!pl.fused)
