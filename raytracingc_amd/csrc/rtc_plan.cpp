@@ -296,6 +296,7 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         if (p.merge) {
             scratch(kRead, L.pixItem, L.geoColor);
             scratch(kRead, L.geoColor, L.end);
+            put(kResGeoSet, kRead, p.geoSet, 0, 1); /* the counts: an entry's item */
         }
         colors();
         if (r.segments)
