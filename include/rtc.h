@@ -315,6 +315,12 @@ int rtc_probe_ray_sphere(const Ray *rays, const Sphere *spheres, size_t n, int *
 int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_t n, vec3 *out);                  /* raytracing.c:151 */
 int rtc_probe_random(const unsigned int *seeds, size_t n, int draws, float *uniform, float *normal,
                      vec3 *direction);                                                                  /* moremath.c:89-108 */
+/* The sky kernel's per-pixel sun skip (no reference counterpart; raytracing.c:155-158 is what it must reproduce): vanish[i]
+ * = 1 where the sun term is proved below half an ulp of every colour component, and out[i] = getEnvironmentLight
+ * evaluated with that skip (equal to rtc_probe_environment's value for every ray). */
+int rtc_probe_sun_vanish(const Ray *rays, const Scene *scenes, size_t n, int *vanish, vec3 *out);
+/* The bound the skip compares focus * log2(x) with (host only; -inf: the scene's colours or sun admit no skip). */
+int rtc_env_vanish_limit(const Scene *scene, double *limit);
 /* Soundness probe of the bounce-ray cluster culling (no reference counterpart; raytracing.c:186-214 is the
  * per-triangle test it must never contradict): clusters `tris` as rtc_scene_upload does and, for every ray and
  * every cluster ball (8 triangles) and chunk ball (32 clusters, scenes of more than one chunk), counts [0] hits

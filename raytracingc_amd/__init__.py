@@ -421,6 +421,25 @@ def getEnvironmentLight(rays: np.ndarray, scenes: np.ndarray) -> np.ndarray:
     return out
 
 
+def sun_vanish_probe(rays: np.ndarray, scenes: np.ndarray):
+    """The sky kernel's per-pixel sun skip on the GPU: (vanish int32 [n], environment float32 [n, 3] evaluated with it)."""
+    r = np.ascontiguousarray(rays, RAY_DT)
+    s = np.ascontiguousarray(scenes, SCENE_DT)
+    n = len(r)
+    v = np.zeros(n, np.int32)
+    out = np.zeros((n, 3), np.float32)
+    check(lib().rtc_probe_sun_vanish(_ptr(r), _ptr(s), n, _ptr(v), _ptr(out)), "rtc_probe_sun_vanish")
+    return v, out
+
+
+def env_vanish_limit(scene) -> float:
+    """The bound on focus * log2(x) below which the sky kernel skips the sun term (host only; -inf: never)."""
+    s = np.ascontiguousarray(scene, SCENE_DT).reshape(1)
+    out = C.c_double(0.0)
+    check(lib().rtc_env_vanish_limit(_ptr(s), C.byref(out)), "rtc_env_vanish_limit")
+    return out.value
+
+
 def random_sequences(seeds: np.ndarray, draws: int):
     """moremath.c:89-108 on the GPU: per seed, `draws` x RandomValue, x RandomValueNormalDistrubtion and
     x RandomDiretion, each sequence restarted from the seed."""

@@ -141,7 +141,7 @@ EXPORTS = [
     "rtc_deinterleave_async", "rtc_deinterleave_bands_async", "rtc_copy_async", "rtc_copy_d2h_dma", "rtc_copy_rows_d2h_dma", "rtc_host_register",
     "rtc_host_unregister", "rtc_plan_sim_create", "rtc_plan_sim_launch", "rtc_plan_sim_release", "rtc_frame_loop", "rtc_frame_loop_cameras", "rtc_dma_pending", "rtc_dma_debug_inflight",
     "rtc_probe_ray_triangle", "rtc_probe_ray_sphere", "rtc_probe_environment", "rtc_probe_random",
-    "rtc_probe_cluster_bound",
+    "rtc_probe_cluster_bound", "rtc_probe_sun_vanish", "rtc_env_vanish_limit",
 ]
 
 _lib = None
@@ -221,6 +221,9 @@ def lib() -> C.CDLL:
     L.rtc_probe_environment.argtypes = [vp, vp, sz, vp]
     L.rtc_probe_random.argtypes = [vp, sz, ip, vp, vp, vp]
     L.rtc_probe_cluster_bound.argtypes = [vp, ip, vp, sz, vp]
+    if hasattr(L, "rtc_probe_sun_vanish"):  # (absent from libraries of earlier rounds loaded for A/B timing)
+        L.rtc_probe_sun_vanish.argtypes = [vp, vp, sz, vp, vp]
+        L.rtc_env_vanish_limit.argtypes = [vp, vp]
     _lib = L
     return L
 

@@ -211,6 +211,8 @@ struct EnvParams {
     V3 sun, horizon, zenith, ground;
     float focus, intensity;
     bool sunSkip; /* env_sun_skippable(focus, intensity) */
+    /* sun_vanishes' limit on focus * log2(x) (env_vanish_limit; -inf: never) */
+    double vanishLim;
     /* powf tables: every kernel that evaluates the environment points them at its LDS copies (PowTablesLds; round 4:
      * no null-table branch to glibc's constants in global memory, whose code the sky kernel paid for in spills) */
     const double (*log2tab)[2];
@@ -273,8 +275,45 @@ __host__ __device__ __forceinline__ bool env_sun_skippable(float focus, float in
 /* getEnvironmentLight (raytracing.c:151-160).  A powf whose value is known for every live lane of the wave is
  * not evaluated (a wave-uniform branch, values unchanged): skyGradientT when smoothstep gives +0 (powf(+0, .35)
  * = +0) -- rays below the horizon --, the sun term as env_sun_skippable says. */
+/* Round 6: the sun term provably adds nothing to any colour component.  With every component of the ground, horizon and
+ * zenith colours >= m > 0, each component of lerp(ground, lerp(horizon, zenith, a), b) = g (1 - b) + s b (a, b in [0, 1];
+ * fl(1 - b) >= (1 - b)(1 - u), each product and sum rounded) is >= m (1 - u)^6, so its exponent is at least
+ * E = floor(log2(m (1 - 2^-20))) and the spacing above it at least 2^(E - 23): with H = 2^(E - 24), a sun term
+ * 0 <= sv < H leaves every component's sum e + sv == e (round to nearest).  sv = fl(powf(x, focus) * intensity) for
+ * sunMask = 1, and glibc's powf is exp2 of the double ylogx = focus * log2(x) it computes (powf_log2 and the same product:
+ * the bits sun_vanishes compares) with a relative error below 2^-23 (its exp2 polynomial ~2^-30, the float rounding
+ * 2^-24); with the product's rounding sv <= 2^ylogx * intensity * (1 + 2^-22).  So ylogx < log2(H / intensity) - 1e-5
+ * (env_vanish_limit, on the host in double) proves sv < H.  Required: focus > 0 and finite (sunSkip), intensity > 0 and
+ * finite, x a normal float in (0, 1), every colour component in [2^-60, 2^60] (no product underflows or overflows; else
+ * the limit is -inf).  Skipping the powf then is the sunKnown skip of a value known to vanish (tests/test_gpu_parity.py
+ * whole frames, tests/test_oracle_env.py the bound against the oracle's environment on every tested direction). */
+__host__ __device__ inline double env_vanish_limit(float focus, float intensity, const float col[9])
+{
+    if (!(focus > 0.f) || !(intensity > 0.f) || !(focus < 3.0e38f) || !(intensity < 3.0e38f))
+        return -__builtin_inf();
+    double m = 1e300;
+    for (int i = 0; i < 9; ++i) {
+        if (!(col[i] >= 0x1p-60f) || !(col[i] <= 0x1p60f))
+            return -__builtin_inf();
+        m = col[i] < m ? (double)col[i] : m;
+    }
+    int E = 0;
+    (void)frexp(m * (1.0 - 0x1p-20), &E); /* m (1 - 2^-20) = f 2^E, f in [0.5, 1): floor(log2) = E - 1 */
+    const double H = ldexp(1.0, (E - 1) - 24);
+    return log2(H / (double)intensity) - 1e-5;
+}
+__device__ __forceinline__ bool sun_vanishes(V3 dir, const EnvParams &s)
+{
+    const float x = fmax0_ref(dot(dir, s.sun));
+    const unsigned ix = __float_as_uint(x);
+    if (!(s.vanishLim > -1e300) || !(dir.y < 0.f) || ix < 0x00800000u || ix >= 0x3f800000u)
+        return false;
+    const double ylogx = (double)s.focus * rtcmath::powf_log2<true>(ix, s.log2tab);
+    return ylogx < s.vanishLim;
+}
+
 template <bool kMissTerm>
-__device__ __forceinline__ V3 environment_t(V3 dir, const EnvParams &s)
+__device__ __forceinline__ V3 environment_t(V3 dir, const EnvParams &s, bool sunVanish = false)
 {
     const float skyArg = smoothstep_k<kSkyStep>(-dir.y);
     float skyGradientT = 0.f;
@@ -290,8 +329,9 @@ __device__ __forceinline__ V3 environment_t(V3 dir, const EnvParams &s)
     float groundToSkyT = smoothstep_k<kGroundStep>(-dir.y);
     float sunMask = dir.y < 0.f ? 1.f : 0.f;
     float sv = __builtin_copysignf(0.f, s.intensity);
-    const bool sunKnown = s.sunSkip && __float_as_uint(sunArg) != 0x80000000u && /* powf(-0, odd) = -0 */
-                          (sunArg == 0.f || (sunMask == 0.f && sunArg <= 1.f));
+    const bool sunKnown = (s.sunSkip && __float_as_uint(sunArg) != 0x80000000u && /* powf(-0, odd) = -0 */
+                           (sunArg == 0.f || (sunMask == 0.f && sunArg <= 1.f))) ||
+                          sunVanish;
     if (__any(!sunKnown)) {
         const float sun = pow_ref(sunArg, s.focus, s) * s.intensity;
         sv = sun * sunMask;
@@ -310,9 +350,9 @@ __device__ __forceinline__ V3 environment(V3 dir, const EnvParams &s) { return e
  * is +-0 either way and sum + (+-0) = sum; a NaN x passes through both adds unchanged.  So the two adds by zero per
  * component are not executed: the reference's values, bit for bit, with 6 fewer VALU operations per sky sample.
  * Otherwise (a sun term computed) m = 0 + e, the reference's operations as they are. */
-__device__ __forceinline__ V3 environment_miss_term(V3 dir, const EnvParams &s)
+__device__ __forceinline__ V3 environment_miss_term(V3 dir, const EnvParams &s, bool sunVanish = false)
 {
-    return environment_t<true>(dir, s);
+    return environment_t<true>(dir, s, sunVanish);
 }
 
 /* EPSILON is the double 0.001 (scene.h:37); for any float v, v < 0.001 <=> v < 0.001f and

@@ -67,6 +67,41 @@ __global__ void probe_env_kernel(const Ray *rays, const Scene *scenes, size_t n,
     out[i] = vec3{c.x, c.y, c.z};
 }
 
+__host__ __device__ static double rtc_env_vanish_limit_of(const Scene &s)
+{
+    const float col[9] = {s.groundColor.x,     s.groundColor.y,     s.groundColor.z,
+                          s.skyColorHorizon.x, s.skyColorHorizon.y, s.skyColorHorizon.z,
+                          s.skyColorZenith.x,  s.skyColorZenith.y,  s.skyColorZenith.z};
+    return env_vanish_limit(s.sunFocus, s.sunIntensity, col);
+}
+
+/* the sky kernel's per-pixel sun skip (rtc_device.h sun_vanishes) and the environment evaluated with it */
+__global__ void probe_vanish_kernel(const Ray *rays, const Scene *scenes, size_t n, int *vanish, vec3 *out)
+{
+    __shared__ PowTablesLds sPow;
+    sPow.fill(threadIdx.x);
+    __syncthreads();
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const Scene s = scenes[i];
+    EnvParams e{};
+    sPow.attach(e);
+    e.sun = v3(s.normalizedSunDirection);
+    e.horizon = v3(s.skyColorHorizon);
+    e.zenith = v3(s.skyColorZenith);
+    e.ground = v3(s.groundColor);
+    e.focus = s.sunFocus;
+    e.intensity = s.sunIntensity;
+    e.sunSkip = env_sun_skippable(e.focus, e.intensity);
+    e.vanishLim = rtc_env_vanish_limit_of(s);
+    const V3 d = v3(rays[i].dir);
+    const bool v = sun_vanishes(d, e);
+    vanish[i] = v ? 1 : 0;
+    const V3 c = environment_t<false>(d, e, v);
+    out[i] = vec3{c.x, c.y, c.z};
+}
+
 __global__ void probe_random_kernel(const unsigned *seeds, size_t n, int draws, float *uni, float *nrm, vec3 *dirs)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -232,6 +267,37 @@ extern "C" int rtc_probe_environment(const Ray *rays, const Scene *scenes, size_
     hipLaunchKernelGGL(probe_env_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy(out, dout, n * sizeof(vec3), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int rtc_probe_sun_vanish(const Ray *rays, const Scene *scenes, size_t n, int *vanish, vec3 *out)
+{
+    if (int rc = probe_prelude())
+        return rc;
+    if (n == 0)
+        return 0;
+    Scratch sc;
+    Ray *dr;
+    Scene *ds;
+    int *dv;
+    vec3 *dout;
+    ALLOC_IN(dr, rays, n * sizeof(Ray));
+    ALLOC_IN(ds, scenes, n * sizeof(Scene));
+    ALLOC_OUT(dv, n * sizeof(int));
+    ALLOC_OUT(dout, n * sizeof(vec3));
+    hipLaunchKernelGGL(probe_vanish_kernel, dim3(probe_blocks(n)), dim3(256), 0, nullptr, dr, ds, n, dv, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(vanish, dv, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, dout, n * sizeof(vec3), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+/* the limit sun_vanishes compares with (host code: no device needed) */
+extern "C" int rtc_env_vanish_limit(const Scene *scene, double *limit)
+{
+    if (!scene || !limit)
+        return RTC_EINVAL;
+    *limit = rtc_env_vanish_limit_of(*scene);
     return 0;
 }
 

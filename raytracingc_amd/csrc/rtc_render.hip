@@ -1366,13 +1366,16 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
             for (int s = 0; s < P.spp; ++s)
                 acc = add(acc, mul(l, P.invSpp));
         } else {
+            /* the sun term provably below half an ulp of every colour component for this pixel (sun_vanishes, a
+             * function of the pixel's direction and the launch's environment) */
+            const bool vanish = sun_vanishes(dir, P.env);
 #pragma unroll 2
             for (int s = 0; s < P.spp; ++s) {
 #if defined(RTC_AB_CHEAP_ENV_SKY) && defined(RTC_EXPERIMENT) /* timing experiment only (the environment's cost) */
                 const V3 l = lerp(P.env.horizon, P.env.zenith, fmaxf(dir.y + (float)s * 1e-9f, 0.f));
 #else
                 /* raytracing.c:291 with rayColor (1, 1, 1): 0 + environment (environment_miss_term: acc starts at +0) */
-                const V3 l = environment_miss_term(dir, P.env);
+                const V3 l = environment_miss_term(dir, P.env, vanish);
 #endif
                 acc = add(acc, mul(l, P.invSpp)); /* main.c:99 */
             }
@@ -1429,6 +1432,9 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
+#ifndef RTC_SUN_VANISH
+#define RTC_SUN_VANISH 1 /* (A/B switch, round 6) */
+#endif
 #ifndef RTC_SKY_MERGE
 #define RTC_SKY_MERGE 1 /* (A/B switch, round 6) */
 #endif
@@ -2370,6 +2376,9 @@ static EnvParams env_of(const Scene &s)
     e.focus = s.sunFocus;
     e.intensity = s.sunIntensity;
     e.sunSkip = env_sun_skippable(e.focus, e.intensity);
+    const float col[9] = {e.ground.x, e.ground.y, e.ground.z, e.horizon.x, e.horizon.y, e.horizon.z,
+                          e.zenith.x, e.zenith.y, e.zenith.z};
+    e.vanishLim = RTC_SUN_VANISH && e.sunSkip ? env_vanish_limit(e.focus, e.intensity, col) : -INFINITY;
     return e;
 }
 
