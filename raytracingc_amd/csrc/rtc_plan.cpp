@@ -127,8 +127,7 @@ void plan_launch(const State &s, const Request &r, Plan &p)
         L.mask = 0;
         L.pixMask = L.mask + maskBytes;
         L.weight = L.pixMask + p.tiles * 8;
-        L.tileW = L.weight + p.blocks * 4;
-        L.order = L.tileW + p.tiles * 4;
+        L.order = L.weight + p.blocks * 4;
         L.geoList = L.order + (p.blocks + 4 + (size_t)kGeoLists * kGeoCountStride) * 4;
         L.superMask = align_up(L.geoList + (size_t)kGeoLists * p.geoCap * 4, 8);
         L.pixItem = align_up(L.superMask + superBytes, 256);
@@ -285,7 +284,7 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         put(kResPrim, kRead, (unsigned long long)p.half, 0, 1);
         if (p.superCull)
             scratch(kRead, L.superMask, L.end);
-        scratch(kWrite, L.mask, L.order); /* mask, pixMask, weight, tileW */
+        scratch(kWrite, L.mask, L.order); /* mask, pixMask, weight */
         if (p.chain) {
             scratch(kWrite, L.geoList, L.superMask);
             if (p.merge)
@@ -295,7 +294,7 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         }
         break;
     case kKSky:
-        scratch(kRead, L.pixMask, L.order);
+        scratch(kRead, L.pixMask, L.weight);
         if (p.merge) {
             scratch(kRead, L.pixItem, L.geoColor);
             scratch(kRead, L.geoColor, L.end);
@@ -328,7 +327,7 @@ int kernel_footprint(const Plan &p, const Request &r, int kernel, Footprint *out
         colors();
         break;
     case kKOrder:
-        scratch(kRead, L.weight, L.tileW);
+        scratch(kRead, L.weight, L.order);
         scratch(kWrite, L.order, L.order + (p.blocks + 4) * 4);
         break;
     case kKRender:

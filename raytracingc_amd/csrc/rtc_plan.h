@@ -94,7 +94,7 @@ struct Request {
 
 /* byte offsets inside one scratch slot (the tile cull's outputs, rtc_render.hip) */
 struct Layout {
-    size_t mask, pixMask, weight, tileW, order, geoList, superMask;
+    size_t mask, pixMask, weight, order, geoList, superMask;
     size_t pixItem;  /* per pixel (tile * 64 + bit) of the geometry pixels: its item (merged sky pass) */
     size_t geoColor; /* per item: its Color bytes (merged sky pass) */
     size_t end;

@@ -867,10 +867,16 @@ __global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned lo
     }
 }
 
+/* Outputs: pixMask (every tile: its pixels with a candidate) and, for the split launch (P.geoList), the candidate words
+ * of the workgroups with a surviving triangle and the geometry-pixel lists: rtc_render_chain reads the words of the
+ * tiles its items lie in, the sky pass pixMask alone.  Round 6: a split launch no longer writes the zero words of the
+ * workgroups without a survivor (most of a sky-heavy frame), a per-tile pixel count or the workgroup weights (only
+ * rtc_order_blocks reads those, before the one-lane-per-pixel kernel): see DESIGN §3.6 for the bytes. */
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
-                                                       unsigned *__restrict__ weight, unsigned *__restrict__ tileW,
+                                                       unsigned *__restrict__ weight,
                                                        unsigned long long *__restrict__ pixMask)
 {
+    const bool split = P.geoList != nullptr; /* (uniform) */
     if (KARG(cullPrio)) /* (RenderParams::cullPrio) */
         __builtin_amdgcn_s_setprio(3);
     __shared__ unsigned wgWeight, wgAny;
@@ -913,13 +919,11 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
     const int tile = wave_tile(bx, by);
     unsigned long long *out = mask + (size_t)tile * P.maskWords;
     if (!wgAny) { /* workgroup-uniform: no triangle survives for any of its pixels (most of a sky-heavy frame) */
-        for (int w = lane; w < P.maskWords; w += 64)
+        for (int w = lane; !split && w < P.maskWords; w += 64)
             out[w] = 0ull;
-        if (lane == 0) {
-            tileW[tile] = 0u;
+        if (lane == 0)
             pixMask[tile] = 0ull;
-        }
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0 && !split)
             weight[blockIdx.y * gridDim.x + blockIdx.x] = 0u;
         CSTAMP(c9);
         CREC(blockIdx.y * gridDim.x + blockIdx.x, c0, c1, c9, 0, 0, 0, 0);
@@ -961,13 +965,11 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         if (lane == 0)
             out[w] = bits;
     }
-    /* tile and workgroup weights: pixels with at least one candidate (they do the bounce work); a tile has a
-     * non-empty candidate list exactly when its weight is > 0 */
+    /* the tile's pixels with at least one candidate (they do the bounce work); a tile has a non-empty candidate list
+     * exactly when one of them is set */
     const unsigned long long b = __ballot(anyCand);
-    if (lane == 0) {
-        tileW[tile] = (unsigned)__popcll(b);
+    if (lane == 0)
         pixMask[tile] = b;
-    }
     if (P.geoList && b) {
         /* this tile's geometry pixels, appended to sub-list tile % kGeoLists (rtc_render_chain's work) */
         const auto append = [&](unsigned long long gb, int l) {
@@ -986,11 +988,13 @@ __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned
         };
         append(b, tile % kGeoLists);
     }
-    if (lane == 0 && b)
-        atomicAdd(&wgWeight, (unsigned)__popcll(b));
-    __syncthreads();
-    if (threadIdx.x == 0)
-        weight[blockIdx.y * gridDim.x + blockIdx.x] = wgWeight;
+    if (!split) { /* the one-lane-per-pixel kernel's workgroup order (rtc_order_blocks) */
+        if (lane == 0 && b)
+            atomicAdd(&wgWeight, (unsigned)__popcll(b));
+        __syncthreads();
+        if (threadIdx.x == 0)
+            weight[blockIdx.y * gridDim.x + blockIdx.x] = wgWeight;
+    }
     CSTAMP(c6);
 #ifdef RTC_DIAG
     CREC(blockIdx.y * gridDim.x + blockIdx.x, c0, c1, c6, 1, dPre, dLoop, dCand);
@@ -1310,7 +1314,7 @@ __device__ __forceinline__ void wave_lds_sync()
  * the 1/4 share took 3.5 % longer with them, profiles/r04_zd_ab_sky_wg.log). */
 template <int kSkyWaves>
 __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky_rows(
-    RenderParams P, const unsigned *__restrict__ tileW)
+    RenderParams P)
 {
     static_assert(kSkyWaves == 4 || kSkyWaves == 1, "one or four row strips per workgroup");
     __shared__ PowTablesLds sPow;
@@ -1328,7 +1332,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
     int t = 0;
     if (inFrame) {
         t = (r >> 3) * (P.blocksX * 2) + (x >> 3);
-        geo = tileW[t] > 0 && ((P.pixMask[t] >> (((r & 7) << 3) | (x & 7))) & 1ull);
+        geo = ((P.pixMask[t] >> (((r & 7) << 3) | (x & 7))) & 1ull) != 0ull;
     }
     const bool valid = inFrame && !geo; /* a sky pixel: this kernel renders it */
     /* merged (P.geoColor): the geometry kernel has finished; its pixels' bytes are written here too, so every strip is
@@ -2508,14 +2512,13 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
     P.primX = s->primX + (size_t)half * s->primStride;
     P.blocksX = (int)pl.gridX;
     unsigned long long *mask = nullptr, *pixMask = nullptr, *superMask = nullptr;
-    unsigned *weight = nullptr, *tileW = nullptr;
+    unsigned *weight = nullptr;
     int *order = nullptr;
     if (pl.cull) {
         unsigned char *slot = s->scratch + pl.slotOffset;
         mask = (unsigned long long *)(slot + pl.lay.mask);
         pixMask = (unsigned long long *)(slot + pl.lay.pixMask);
         weight = (unsigned *)(slot + pl.lay.weight);
-        tileW = (unsigned *)(slot + pl.lay.tileW);
         order = (int *)(slot + pl.lay.order);
         superMask = (unsigned long long *)(slot + pl.lay.superMask);
         if (pl.merge) {
@@ -2594,7 +2597,7 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             break;
         case rtcplan::kKTileCull:
             HIP_TRY(launch_stop(rtc_tile_cull, grid, dim3(kBlock), (size_t)s->maskWords * sizeof(unsigned long long), os, ev,
-                                P, mask, weight, tileW, pixMask));
+                                P, mask, weight, pixMask));
             break;
         case rtcplan::kKSky: {
             if (s->timing)
@@ -2602,10 +2605,9 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             const bool skyWide = pl.smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
             if (skyWide)
                 hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0, os,
-                                   P, (const unsigned *)tileW);
+                                   P);
             else
-                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, os, P,
-                                   (const unsigned *)tileW);
+                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, os, P);
             HIP_TRY(hipGetLastError());
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky1, os));
