@@ -1436,12 +1436,6 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
  * pipelined, prepare, cull and run their geometry kernel on the two cull streams.  Round 4 raised it
  * from 400 k to 600 k pixels so that the 1080p 1/4 share (518 k) is one: 0.137 -> 0.117 ms per pipelined share; the
  * 1/2 share and the 4K 1/8 share (1.04 M) measured no better that way (tools/scale_probe.py, profiles/r04_y_*) */
-#ifndef RTC_PRIM_PREFETCH
-#define RTC_PRIM_PREFETCH 1 /* (A/B switch, round 6) */
-#endif
-#ifndef RTC_XCD_RUNS
-#define RTC_XCD_RUNS 1 /* (A/B switch, round 6) */
-#endif
 #ifndef RTC_SUN_VANISH
 #define RTC_SUN_VANISH 1 /* (A/B switch, round 6) */
 #endif
@@ -1840,21 +1834,14 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
     const DevPrimX *const primX = KARG(primX);
     for (int w = 0; w < maskWords; ++w) {
         unsigned long long m = w == 0 ? m0 : w == 1 ? m1 : KCONST(mask)[w];
-        if (!m)
-            continue;
-        /* two loads of known address space (LDS, or a scalar load): a pointer that may be either would be read with
-         * flat loads, whose wait also covers the wave's pending slot stores.  Round 6: the next candidate's record is
-         * requested before this one is tested (RTC_PRIM_PREFETCH), so its LDS round trip overlaps the test. */
-        int t = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        DevPrimF F = staged ? sF[t] : KLOAD(primF, t);
-        for (;;) {
-            const bool more = m != 0ull;
-            const int tn = more ? w * 64 + __builtin_ctzll(m) : t;
+        while (m) {
+            const int t = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            DevPrimF Fn;
-            if (RTC_PRIM_PREFETCH)
-                Fn = staged ? sF[tn] : KLOAD(primF, tn);
+            /* two loads of known address space (LDS, or a scalar load): a pointer that may be either would be
+             * read with flat loads, whose wait also covers the wave's pending slot stores.  (Requesting the next
+             * candidate's record before testing this one, round 6: 1080p shares 2-3 % longer, the frame unchanged,
+             * profiles/r06_i_ab_cull_trim_xcd_runs_prefetch.log.) */
+            const DevPrimF F = staged ? sF[t] : KLOAD(primF, t);
             if (!prim_backfacing(dir, F) && prim_pass(dir, F) && !(dot(dir, V3{F.nx, F.ny, F.nz}) >= 0.f)) {
                 /* the reference's arithmetic (raytracing.c:189-208) */
                 const DevPrimX X = KLOAD(primX, t);
@@ -1871,13 +1858,6 @@ __device__ __forceinline__ void closest_primary_listed_lds(const RenderParams &P
                     }
                 }
             }
-            if (!more)
-                break;
-            t = tn;
-            if (RTC_PRIM_PREFETCH)
-                F = Fn;
-            else
-                F = staged ? sF[t] : KLOAD(primF, t);
         }
     }
 }
@@ -1958,15 +1938,10 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
      * fills its tail -- and small shares 17-28 % longer.  Items grouped by XCD, round 6 -- XCD group b % 8 taking the
      * (b % 8)-th eighth of the list, so that a tile's neighbouring pixels share an L2: frame 0.333 -> 0.358 ms, 1/8 share
      * 0.068 -> 0.079 ms, profiles/r06_c_ab_xcd_items_readlane_cull.log.) */
-    /* Round 6: the workgroups of one XCD (b and b + 8 share one: round-robin dispatch) own runs of G / 8 consecutive
-     * items in every round of G items (G = gridDim.x; own = (b % 8) * G / 8 + b / 8), so the pixels of a tile row -- one
-     * tile's geometry pixels are consecutive items -- are rendered under one L2: their Color bytes merge into whole
-     * sectors before write-back and their tile's candidate words are fetched once per tile, not once per XCD.  The
-     * rounds still interleave every XCD across the whole list (round 6's contiguous eighths per XCD: frame +7 %). */
-    const int own = RTC_XCD_RUNS && (gridDim.x & 7u) == 0u
-                        ? (int)((blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3))
-                        : (int)blockIdx.x;
-    const auto next_item = [&]() { return own + atomicAdd(&sWork, 1) * (int)gridDim.x; };
+    /* (Runs of G / 8 consecutive items per XCD in every round of G = gridDim.x items, round 6 -- a tile's pixels under
+     * one L2, so that their Color bytes merge before write-back: 1080p 1/4 and 1/8 shares 2-3 % longer, fsuzane +1 %,
+     * profiles/r06_i_ab_cull_trim_xcd_runs_prefetch.log.) */
+    const auto next_item = [&]() { return (int)blockIdx.x + atomicAdd(&sWork, 1) * (int)gridDim.x; };
     if (lane == 0)
         nextIt = next_item();
     /* (the launch constants below that are used once per item, window or escaped bounce are re-read from the kernarg

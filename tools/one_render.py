@@ -30,6 +30,21 @@ if v in bench.WORKLOADS:
     ds.close()
     print(v, "rendered", reps)
     sys.exit(0)
+if v in ("share4o", "share8o", "fullo"):
+    # pipelined launches like tools/scale_probe.py overlap: rank 0's share of N = 4 / 8, or the whole frame
+    import torch
+
+    n = {"share4o": 4, "share8o": 8, "fullo": 1}[v]
+    cfg = rt.RenderConfig(1920, 1080, 64, 10, True, overlap=True, row_stride=n)
+    ds = rt.DeviceScene(tris, None, device=0)
+    out = torch.empty((1080, 1920, 3), dtype=torch.uint8, device="cuda:0")
+    s = torch.cuda.Stream()
+    for _ in range(reps):
+        ds.render_rows_async(rt.default_scene(), rt.camera_basis(), cfg, out.data_ptr(), None, None, s.cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    print(v, "rendered", reps)
+    sys.exit(0)
 cfg = {"faithful": rt.RenderConfig(1920, 1080, 64, 10, True),
        "nocull": rt.RenderConfig(1920, 1080, 64, 10, True, tile_cull=False), "mb1": rt.RenderConfig(1920, 1080, 64, 1, True),
        "hoist": rt.RenderConfig(1920, 1080, 64, 10, True, hoist=True),
