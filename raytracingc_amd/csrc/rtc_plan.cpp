@@ -76,11 +76,12 @@ void plan_launch(const State &s, const Request &r, Plan &p)
     p.chainOnCs = p.overlap && (p.smallShare || px > kInlineSumPixels);
     /* Round 6: a pipelined launch on the alternating streams runs its sky pass AFTER its geometry kernel
      * (which then writes each pixel's colour into a per-item word, not into Color) and the sky pass writes every pixel of
-     * the frame in whole 64-B lines -- no partial line written back from up to eight XCDs' L2s.  In the pipelined steady
-     * state this sky pass runs beside the next frame's geometry kernel, as the previous one did beside this frame's.
-     * Small shares only: whole 1080p frames took 19 % longer with it (0.398 vs 0.336 ms: the sky pass no longer hides
-     * beside its own frame's geometry kernel), 1080p 1/4 shares 4 % less (0.110 vs 0.115 ms), 1/8 shares and C3 fsuzane
-     * the same (profiles/r06_f_ab_merged_sky.log). */
+     * the frame in whole 64-B lines.  In the pipelined steady state this sky pass runs beside the next frame's geometry
+     * kernel, as the previous one did beside this frame's.  Small shares only: whole 1080p frames took 19 % longer with it
+     * (0.398 vs 0.336 ms: the sky pass no longer hides beside its own frame's geometry kernel), 1080p 1/4 shares 4 % less
+     * (0.110 vs 0.115 ms), 1/8 shares and C3 fsuzane the same (profiles/r06_f_ab_merged_sky.log).  It does not save
+     * bytes: the per-item words are as scattered as the Color triples were (1/4 share: geometry kernel WRITE_SIZE 452 ->
+     * 601 KB, sky 1465 -> 1519 KB, profiles/r06_j_pmc_writes.log); the gain is the schedule. */
     p.merge = p.chainOnCs && p.smallShare && !r.noMerge;
     p.needCst2 = p.chainOnCs && !s.cst2;
     if (p.needCst2)

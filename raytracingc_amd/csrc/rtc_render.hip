@@ -871,7 +871,8 @@ __global__ __launch_bounds__(64) void rtc_super_cull(RenderParams P, unsigned lo
  * of the workgroups with a surviving triangle and the geometry-pixel lists: rtc_render_chain reads the words of the
  * tiles its items lie in, the sky pass pixMask alone.  Round 6: a split launch no longer writes the zero words of the
  * workgroups without a survivor (most of a sky-heavy frame), a per-tile pixel count or the workgroup weights (only
- * rtc_order_blocks reads those, before the one-lane-per-pixel kernel): see DESIGN §3.6 for the bytes. */
+ * rtc_order_blocks reads those, before the one-lane-per-pixel kernel): WRITE_SIZE per 1080p launch 2.13 -> 0.88 MB, the
+ * frame unchanged (profiles/r06_j_pmc_writes.log, r06_i_ab_cull_trim_xcd_runs_prefetch.log). */
 __global__ __launch_bounds__(kBlock) void rtc_tile_cull(RenderParams P, unsigned long long *__restrict__ mask,
                                                        unsigned *__restrict__ weight,
                                                        unsigned long long *__restrict__ pixMask)
