@@ -131,7 +131,13 @@ class Scenario:
             o, k = kernel_ops[i]
             self.accesses.append((o, res, acc, ident, lo, hi, key, self.n, k))
         self.n += 1
+        self.last_ops = [tuple(int(v) for v in self.ops[4 * i: 4 * i + 4]) for i in range(nops)]
         return {"slot": int(info[2]), "alt": bool(info[3]), "overlap": bool(info[4]), "offset": int(info[5])}
+
+    def kernel_order(self):
+        """The last launch's kernels in enqueue order, as (name, stream)."""
+        names = {0: "caller", 1: "cull0", 2: "cull1", 3: "side"}
+        return [(KNAMES[k], names[st]) for kind, st, _, k in self.last_ops if kind == KERNEL]
 
     def hazards(self, limit=5):
         """Pairs of kernels of different launches (or the same one) that touch the same memory without an order."""
@@ -304,5 +310,12 @@ def test_plan_shapes():
         assert small["overlap"] and not small["alt"]  # small whole frames keep the caller's stream
         share = sc.launch(_desc(1920, 1080, 64, 3, 8, 0, OVERLAP), 0x7f001000, 0x5000, 0, False, CAMS[0], ENVS[0])
         assert share["overlap"] and share["alt"]
+        # small shares: the merged sky pass follows the geometry kernel
+        ks = [k for k, _ in sc.kernel_order()]
+        assert ks.index("chain") < ks.index("sky") and ("sky", "side") in sc.kernel_order()
+        # whole pipelined frames: the sky pass is enqueued beside the geometry kernel, not after it
+        sc.launch(_desc(1920, 1080, 64, 0, 1, 0, OVERLAP), 0x7f001000, 0x1000, 0, False, CAMS[0], ENVS[0])
+        ks = [k for k, _ in sc.kernel_order()]
+        assert ks.index("sky") < ks.index("chain")
     finally:
         sc.close()
