@@ -12,10 +12,6 @@
 #include <vector>
 
 #include "rtc_layout.h"
-
-#ifndef RTC_SIDE_PRIO_HIGH
-#define RTC_SIDE_PRIO_HIGH 0 /* (A/B switch, round 6) */
-#endif
 #include "rtc_internal.h"
 #include "rtc_hip_util.h"
 
@@ -430,7 +426,7 @@ extern "C" int rtc_scene_upload_with_share(const Triangle *tris, int triCount, c
     if (e == hipSuccess)
         e = hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio);
     if (e == hipSuccess) /* the sky tiles yield to the heavy tiles */
-        e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, RTC_SIDE_PRIO_HIGH ? greatestPrio : leastPrio);
+        e = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, leastPrio);
     if (e == hipSuccess) /* the next frame's cull goes first wherever a CU frees up */
         e = hipStreamCreateWithPriority(&s->cst, hipStreamNonBlocking, greatestPrio);
     if (e == hipSuccess)
