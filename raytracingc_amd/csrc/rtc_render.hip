@@ -1440,6 +1440,9 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
 #ifndef RTC_SUN_VANISH
 #define RTC_SUN_VANISH 1 /* (A/B switch, round 6) */
 #endif
+#ifndef RTC_FUSED_PAIRS
+#define RTC_FUSED_PAIRS 1 /* (A/B switch, round 6) */
+#endif
 #ifndef RTC_SKY_MERGE
 #define RTC_SKY_MERGE 1 /* (A/B switch, round 6) */
 #endif
@@ -1707,7 +1710,25 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         }
         /* table mode: bit j of cm = the j-th live cluster kept (branch-free body over the compacted terms) */
         const int nLive = __popcll(live);
-        if (dense) {
+        /* (round 6) table mode with every lane's pairs fitting the list: the cull and the pair list in one pass over the
+         * live clusters -- each cluster's ballot of the lanes keeping it appends their entries at once, in the same
+         * cluster-major, lane-ascending order as the separate build below */
+        const bool fused = RTC_FUSED_PAIRS && table && nLive * 64 <= kChainPairs; /* (uniform) */
+        if (fused) {
+#pragma unroll 4
+            for (int j = 0; j < nLive; ++j) {
+                const float4 a = W.cl[j][0], b = W.cl[j][1];
+                const ClusterTerms t{V3{a.x, a.y, a.z}, a.w, b.x, b.y};
+                const bool kept = in && !(rhoOk && culled_by(t, dir, rho, dd));
+                tests += kept ? (unsigned)__popc((unsigned)__float_as_int(b.w)) : 0u;
+                const unsigned long long m = __ballot(kept);
+                if (kept)
+                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                        (unsigned short)(lane | (j << 6));
+                n += (int)__popcll(m);
+            }
+        } else if (dense) {
         } else if (in && table) {
             /* (round 6: each live cluster's terms by v_readlane from the lane that computed them instead of these LDS
              * reads -- six VALU readlanes per cluster: chain kernel +3 %, frame +2.4 %, profiles/r06_c_ab_*) */
@@ -1730,7 +1751,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
         constexpr int kCap = kChainPairs;
-        if (dense) {
+        if (dense || fused) {
         } else if (table) {
             /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
              * whenever the next cluster would overflow it */
