@@ -1440,9 +1440,6 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
 #ifndef RTC_SUN_VANISH
 #define RTC_SUN_VANISH 1 /* (A/B switch, round 6) */
 #endif
-#ifndef RTC_FUSED_PAIRS
-#define RTC_FUSED_PAIRS 1 /* (A/B switch, round 6) */
-#endif
 #ifndef RTC_SKY_MERGE
 #define RTC_SKY_MERGE 1 /* (A/B switch, round 6) */
 #endif
@@ -1712,8 +1709,8 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         const int nLive = __popcll(live);
         /* (round 6) table mode with every lane's pairs fitting the list: the cull and the pair list in one pass over the
          * live clusters -- each cluster's ballot of the lanes keeping it appends their entries at once, in the same
-         * cluster-major, lane-ascending order as the separate build below */
-        const bool fused = RTC_FUSED_PAIRS && table && nLive * 64 <= kChainPairs; /* (uniform) */
+         * cluster-major, lane-ascending order as the separate build below (frame -0.7 %, profiles/r06_p_ab_fused_pairs.log) */
+        const bool fused = table && nLive * 64 <= kChainPairs; /* (uniform) */
         if (fused) {
 #pragma unroll 4
             for (int j = 0; j < nLive; ++j) {
