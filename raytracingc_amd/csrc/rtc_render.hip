@@ -1714,8 +1714,10 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
          * live clusters -- each cluster's ballot of the lanes keeping it appends their entries at once, in the same
          * cluster-major, lane-ascending order as the separate build below (frame -0.7 %, profiles/r06_p_ab_fused_pairs.log) */
         const bool fused = table && nLive * 64 <= kChainPairs; /* (uniform) */
-        /* the same for the per-lane culls of later bounces (more than kDenseCullMax live lanes) */
-        const bool fusedG = RTC_FUSED_LATER && !table && !dense && nCl * 64 <= kChainPairs; /* (uniform) */
+        /* the same for the per-lane culls of later bounces (more than kDenseCullMax live lanes; a first bounce without
+         * the table keeps the separate build: fused there, the headline's geometry kernel took 0.8 % longer,
+         * profiles/r06_u_ab_fused_later.log) */
+        const bool fusedG = RTC_FUSED_LATER && !firstBounce && !table && !dense && nCl * 64 <= kChainPairs; /* (uniform) */
         if (fusedG) {
             for (int k = 0; k < nCl; ++k) {
                 const bool kept = in && !(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k]));
