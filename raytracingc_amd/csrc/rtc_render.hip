@@ -1440,9 +1440,6 @@ static_assert(sizeof(SampleSlot) == rtcplan::kSampleSlotBytes, "the planner size
 #ifndef RTC_SUN_VANISH
 #define RTC_SUN_VANISH 1 /* (A/B switch, round 6) */
 #endif
-#ifndef RTC_FUSED_LATER
-#define RTC_FUSED_LATER 1 /* (A/B switch, round 6) */
-#endif
 #ifndef RTC_SKY_MERGE
 #define RTC_SKY_MERGE 1 /* (A/B switch, round 6) */
 #endif
@@ -1714,26 +1711,9 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
          * live clusters -- each cluster's ballot of the lanes keeping it appends their entries at once, in the same
          * cluster-major, lane-ascending order as the separate build below (frame -0.7 %, profiles/r06_p_ab_fused_pairs.log) */
         const bool fused = table && nLive * 64 <= kChainPairs; /* (uniform) */
-        /* the same for the per-lane culls of later bounces (more than kDenseCullMax live lanes; a first bounce without
-         * the table keeps the separate build: fused there, the headline's geometry kernel took 0.8 % longer,
-         * profiles/r06_u_ab_fused_later.log) */
-        const bool fusedG = RTC_FUSED_LATER && !firstBounce && !table && !dense && nCl * 64 <= kChainPairs; /* (uniform) */
-        if (fusedG) {
-            for (int k = 0; k < nCl; ++k) {
-                const bool kept = in && !(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k]));
-                cm |= (unsigned)kept << k;
-                const unsigned long long m = __ballot(kept);
-                if (kept)
-                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
-                        (unsigned short)(lane | (k << 6));
-                n += (int)__popcll(m);
-            }
-            if (in) /* triangles in the clusters kept (only the scene's last cluster has zero records) */
-                tests += (unsigned)__popc(cm) * kClusterSize -
-                         (c0 + nCl == P.clusterCount ? ((cm >> (nCl - 1)) & 1u) : 0u) *
-                             (unsigned)(P.clusterCount * kClusterSize - P.triCount);
-        } else if (fused) {
+        /* (The same fusion for the per-lane culls of later bounces, round 6: fsuzane -1 to -2 %, but the headline's geometry
+         * kernel -- which never takes that path -- 0.8-1.4 % longer from the code it adds, profiles/r06_t / r06_u / r06_v.) */
+        if (fused) {
 #pragma unroll 4
             for (int j = 0; j < nLive; ++j) {
                 const float4 a = W.cl[j][0], b = W.cl[j][1];
@@ -1770,7 +1750,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
         constexpr int kCap = kChainPairs;
-        if (dense || fused || fusedG) {
+        if (dense || fused) {
         } else if (table) {
             /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
              * whenever the next cluster would overflow it */
