@@ -1910,7 +1910,11 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
 }
 
 /* COUNT: the launch asks for segment counters (instrumentation, untimed); without it the counters are compiled out */
-template <bool MULTI, bool COUNT> /* MULTI: more than one chunk of clusters (chunk-level culling, records from global) */
+/* MULTI: more than one chunk of clusters (chunk-level culling, records from global).  DEFER (round 6): the launch may give
+ * items deferred sample slots (P.sampleCap > 0: joined whole frames); without it every item sums in-kernel and the slot
+ * code is not in the kernel -- the pipelined launches' instantiation, whose registers and schedule are then those of the
+ * in-kernel sums alone.  Counting launches always take DEFER. */
+template <bool MULTI, bool COUNT, bool DEFER>
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
@@ -2057,7 +2061,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             for (int w = 0; w < P.maskWords; ++w)
                 L += (unsigned)__popcll(mask[w]);
         const unsigned seed = (unsigned)(x + y * KARG(width)); /* main.c:95 */
-        const bool deferred = it < P.sampleCap; /* wave-uniform */
+        const bool deferred = DEFER && it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
         if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
             closest_primary_listed_lds(P, pdir, prim, mask, m0, m1, sPF, pfStaged);
@@ -2643,14 +2647,17 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, os));
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
+            const bool defer = P.sampleCap > 0;
             if (s->chunkCount > 1 && dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<true, true>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, true, true>, cg, cb, chainDyn, os, ev, P));
             else if (s->chunkCount > 1)
-                HIP_TRY(launch_stop(rtc_render_chain<true, false>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(defer ? launch_stop(rtc_render_chain<true, false, true>, cg, cb, chainDyn, os, ev, P)
+                              : launch_stop(rtc_render_chain<true, false, false>, cg, cb, chainDyn, os, ev, P));
             else if (dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<false, true>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, true, true>, cg, cb, chainDyn, os, ev, P));
             else
-                HIP_TRY(launch_stop(rtc_render_chain<false, false>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(defer ? launch_stop(rtc_render_chain<false, false, true>, cg, cb, chainDyn, os, ev, P)
+                              : launch_stop(rtc_render_chain<false, false, false>, cg, cb, chainDyn, os, ev, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, os));
             break;
