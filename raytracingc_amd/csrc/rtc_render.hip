@@ -1910,11 +1910,13 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
 }
 
 /* COUNT: the launch asks for segment counters (instrumentation, untimed); without it the counters are compiled out */
-/* MULTI: more than one chunk of clusters (chunk-level culling, records from global).  DEFER (round 6): the launch may give
- * items deferred sample slots (P.sampleCap > 0: joined whole frames); without it every item sums in-kernel and the slot
- * code is not in the kernel -- the pipelined launches' instantiation, whose registers and schedule are then those of the
- * in-kernel sums alone.  Counting launches always take DEFER. */
-template <bool MULTI, bool COUNT, bool DEFER>
+/* MULTI: more than one chunk of clusters (chunk-level culling, records from global).  GENERAL (round 6): the launch may give
+ * items deferred sample slots (P.sampleCap > 0: joined whole frames), hoist the primary segments (P.hoist) or read the
+ * primary filter records from global memory (!P.chainPrimF: too large to stage); without it every item sums in-kernel
+ * and traces its primary ray per sample over the staged records, and none of the other code is in the kernel -- the pipelined faithful launches' instantiation, whose registers and schedule are then its own
+ * (without the slot code: frame -0.8 %, chain -1.4 %, 1/8 share -2 %, profiles/r06_w_ab_defer_specialisation.log).
+ * Counting launches always take GENERAL. */
+template <bool MULTI, bool COUNT, bool GENERAL>
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
@@ -1941,7 +1943,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
     const float4 *sRec = S.rec;
     /* the staged primary filter records: always the LDS address (never null), used when P.chainPrimF */
     const DevPrimF *sPF = (const DevPrimF *)(sDyn + (MULTI ? 0 : (size_t)soa_slots(P.clusterCount * kClusterSize) * sizeof(DevTri)));
-    const bool pfStaged = P.chainPrimF != 0;
+    const bool pfStaged = !GENERAL || P.chainPrimF != 0; /* (the fast instantiation runs only with the records staged) */
 #ifdef RTC_DIAG
     if ((threadIdx.x & 63) < kDiagSects)
         s_rtc_sect[threadIdx.x >> 6][threadIdx.x & 63] = 0;
@@ -2061,9 +2063,9 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
             for (int w = 0; w < P.maskWords; ++w)
                 L += (unsigned)__popcll(mask[w]);
         const unsigned seed = (unsigned)(x + y * KARG(width)); /* main.c:95 */
-        const bool deferred = DEFER && it < P.sampleCap; /* wave-uniform */
+        const bool deferred = GENERAL && it < P.sampleCap; /* wave-uniform */
         Closest prim{999999.f, -1};
-        if (P.hoist && P.spp > 0 && P.maxBounce > 0) {
+        if (GENERAL && P.hoist && P.spp > 0 && P.maxBounce > 0) {
             closest_primary_listed_lds(P, pdir, prim, mask, m0, m1, sPF, pfStaged);
             if (counting && lane == 0) {
                 segTraced++;
@@ -2105,7 +2107,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                 Closest c{999999.f, -1};
                 if (first) { /* every live lane: the pixel's primary ray (bounce 0) */
                     if (alive) {
-                        if (P.hoist) {
+                        if (GENERAL && P.hoist) {
                             c = prim;
                         } else {
                             closest_primary_listed_lds(P, dir, c, mask, m0, m1, sPF, pfStaged);
@@ -2647,12 +2649,11 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evHeavy0, os));
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
-            const bool defer = P.sampleCap > 0;
+            const bool defer = P.sampleCap > 0 || P.hoist || !P.chainPrimF; /* (GENERAL) */
             if (s->chunkCount > 1 && dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<true, true, true>, cg, cb, chainDyn, os, ev, P));
-            else if (s->chunkCount > 1)
-                HIP_TRY(defer ? launch_stop(rtc_render_chain<true, false, true>, cg, cb, chainDyn, os, ev, P)
-                              : launch_stop(rtc_render_chain<true, false, false>, cg, cb, chainDyn, os, ev, P));
+            else if (s->chunkCount > 1) /* (multi-chunk scenes never stage the primary records: GENERAL) */
+                HIP_TRY(launch_stop(rtc_render_chain<true, false, true>, cg, cb, chainDyn, os, ev, P));
             else if (dSegments)
                 HIP_TRY(launch_stop(rtc_render_chain<false, true, true>, cg, cb, chainDyn, os, ev, P));
             else
