@@ -1590,7 +1590,7 @@ constexpr int kDenseCullMax = 16;
 static_assert(kDenseCullMax * kChunkClusters <= kChainPairs, "a dense cull's pairs fit the list");
 static_assert(sizeof(ChainWaveLds::cl) >= 64 * sizeof(int), "the dense cull's owner lanes fit W.cl");
 
-template <bool MULTI, bool COUNT>
+template <bool MULTI, bool COUNT, bool HITS>
 __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool alive, bool firstBounce, V3 pos,
                                                      V3 dir, const float4 *__restrict__ sRec, ChainWaveLds &W,
                                                      int lane, unsigned &tests, const DevCluster *__restrict__ sCl)
@@ -1711,9 +1711,26 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
          * live clusters -- each cluster's ballot of the lanes keeping it appends their entries at once, in the same
          * cluster-major, lane-ascending order as the separate build below (frame -0.7 %, profiles/r06_p_ab_fused_pairs.log) */
         const bool fused = table && nLive * 64 <= kChainPairs; /* (uniform) */
-        /* (The same fusion for the per-lane culls of later bounces, round 6: fsuzane -1 to -2 %, but the headline's geometry
-         * kernel -- which never takes that path -- 0.8-1.4 % longer from the code it adds, profiles/r06_t / r06_u / r06_v.) */
-        if (fused) {
+        /* the same for the per-lane culls of later bounces (more than kDenseCullMax live lanes), in the HITS instantiation
+         * only: fsuzane -1 to -2 %, while in the one instantiation of round 6's first try the headline's geometry kernel --
+         * which never takes that path -- took 0.8-1.4 % longer from the code it adds (profiles/r06_t / r06_u / r06_v) */
+        const bool fusedG = HITS && !firstBounce && !table && !dense && nCl * 64 <= kChainPairs; /* (uniform) */
+        if (fusedG) {
+            for (int k = 0; k < nCl; ++k) {
+                const bool kept = in && !(rhoOk && cluster_culled(pos, dir, rho, dd, P.clusters[c0 + k]));
+                cm |= (unsigned)kept << k;
+                const unsigned long long m = __ballot(kept);
+                if (kept)
+                    W.pair[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                        (unsigned short)(lane | (k << 6));
+                n += (int)__popcll(m);
+            }
+            if (in) /* triangles in the clusters kept (only the scene's last cluster has zero records) */
+                tests += (unsigned)__popc(cm) * kClusterSize -
+                         (c0 + nCl == P.clusterCount ? ((cm >> (nCl - 1)) & 1u) : 0u) *
+                             (unsigned)(P.clusterCount * kClusterSize - P.triCount);
+        } else if (fused) {
 #pragma unroll 4
             for (int j = 0; j < nLive; ++j) {
                 const float4 a = W.cl[j][0], b = W.cl[j][1];
@@ -1750,7 +1767,7 @@ __device__ __forceinline__ Closest chain_trace_pairs(const RenderParams &P, bool
         DSECT_END(dc3, 3);
         DSECT_BEGIN(dc4);
         constexpr int kCap = kChainPairs;
-        if (dense || fused) {
+        if (dense || fused || fusedG) {
         } else if (table) {
             /* (lane, live cluster) entries, one per cluster a lane keeps; the list is flushed through the passes
              * whenever the next cluster would overflow it */
@@ -1915,8 +1932,10 @@ __device__ __forceinline__ ChainStage chain_stage(const RenderParams &P, unsigne
  * primary filter records from global memory (!P.chainPrimF: too large to stage); without it every item sums in-kernel
  * and traces its primary ray per sample over the staged records, and none of the other code is in the kernel -- the pipelined faithful launches' instantiation, whose registers and schedule are then its own
  * (without the slot code: frame -0.8 %, chain -1.4 %, 1/8 share -2 %, profiles/r06_w_ab_defer_specialisation.log).
- * Counting launches always take GENERAL. */
-template <bool MULTI, bool COUNT, bool GENERAL>
+ * Counting launches always take GENERAL.  HITS: the fast instantiation of scenes whose bounces often hit again (the
+ * upload's bounce_hit_share above kWgsHitShare, e.g. C3 fsuzane), with the later bounces' one-pass cull and pair build
+ * (chain_trace_pairs); the other scenes' instantiation does not carry that code. */
+template <bool MULTI, bool COUNT, bool HITS, bool GENERAL>
 __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC_CHAIN_WAVES))) void rtc_render_chain(
     RenderParams P)
 {
@@ -2122,7 +2141,7 @@ __global__ __launch_bounds__(kChainBlock) __attribute__((amdgpu_waves_per_eu(RTC
                         maskNext = true;
                     }
                     unsigned t = 0;
-                    c = chain_trace_pairs<MULTI, COUNT>(P, alive, bounce1, pos, dir, sRec, W, lane, t, sCl);
+                    c = chain_trace_pairs<MULTI, COUNT, HITS>(P, alive, bounce1, pos, dir, sRec, W, lane, t, sCl);
                     if (counting && alive) {
                         tests += t;
                         clTests += (unsigned)P.clusterCount;
@@ -2650,15 +2669,19 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
                 HIP_TRY(hipEventRecord(s->evHeavy0, os));
             const dim3 cg((unsigned)(wgsPerCu * s->cuCount)), cb(kChainBlock);
             const bool defer = P.sampleCap > 0 || P.hoist || !P.chainPrimF; /* (GENERAL) */
+            const bool hits = s->chainWgsFull == RTC_CHAIN_WGS_HIT && RTC_CHAIN_WGS_HIT != RTC_CHAIN_WGS_FULL;
             if (s->chunkCount > 1 && dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<true, true, true>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, true, false, true>, cg, cb, chainDyn, os, ev, P));
             else if (s->chunkCount > 1) /* (multi-chunk scenes never stage the primary records: GENERAL) */
-                HIP_TRY(launch_stop(rtc_render_chain<true, false, true>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<true, false, false, true>, cg, cb, chainDyn, os, ev, P));
             else if (dSegments)
-                HIP_TRY(launch_stop(rtc_render_chain<false, true, true>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, true, false, true>, cg, cb, chainDyn, os, ev, P));
+            else if (defer)
+                HIP_TRY(launch_stop(rtc_render_chain<false, false, false, true>, cg, cb, chainDyn, os, ev, P));
+            else if (hits)
+                HIP_TRY(launch_stop(rtc_render_chain<false, false, true, false>, cg, cb, chainDyn, os, ev, P));
             else
-                HIP_TRY(defer ? launch_stop(rtc_render_chain<false, false, true>, cg, cb, chainDyn, os, ev, P)
-                              : launch_stop(rtc_render_chain<false, false, false>, cg, cb, chainDyn, os, ev, P));
+                HIP_TRY(launch_stop(rtc_render_chain<false, false, false, false>, cg, cb, chainDyn, os, ev, P));
             if (s->timing) /* the chain kernel alone (rocprof's rtc_render_chain row) */
                 HIP_TRY(hipEventRecord(s->evHeavy1, os));
             break;

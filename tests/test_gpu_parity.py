@@ -511,6 +511,31 @@ def test_device_scene_reuse_sizes_counters_timing(gpu_available):
     ds.close()
 
 
+def test_pipelined_multi_hit_scene_bit_exact(gpu_available):
+    """A scene whose bounces often hit again (fsuzane: 4 geometry-kernel workgroups per CU) pipelined at 1080p runs the
+    HITS instantiation of rtc_render_chain (the later bounces' one-pass cull and pair build); its frames equal the joined
+    render (the GENERAL instantiation, pinned against the oracle elsewhere) bit for bit, for two cameras."""
+    import torch
+
+    tris, _ = load_tris("fsuzane")
+    scene = rt.default_scene()
+    cams = [rt.camera_basis(), rt.camera_basis((-4.0, -1.9, -5.2), (0.6, -1.0, 1.3), 1.1)]
+    W, H, spp = 1920, 1080, 4
+    ds = rt.DeviceScene(tris, None)
+    assert ds.chain_wgs == 4  # the multi-hit instantiation's scenes
+    st = torch.cuda.Stream()
+    out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    cfg = rt.RenderConfig(W, H, spp, 10, True, overlap=True)
+    for c in cams:
+        ref, _, _ = rt.render(tris, None, scene, c, rt.RenderConfig(W, H, spp, 10, True))
+        for _ in range(2):
+            ds.render_rows_async(scene, c, cfg, out.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref)
+    ds.close()
+
+
 @pytest.mark.parametrize("size", [(256, 144, 8), (1920, 1080, 4)])
 @pytest.mark.parametrize("variant", [{}, {"hoist": True}, {"chain_inline": True}])
 def test_overlapped_frames_bit_exact(variant, size, gpu_available):
