@@ -1313,7 +1313,9 @@ __device__ __forceinline__ void wave_lds_sync()
  * workgroup: 1, or 4 for small shares of more than 400 k pixels (one-wave workgroups fill the registers and wave slots
  * the co-resident chain workgroups leave free at a finer grain -- whole frames -1 %, the 1080p 1/8 share -2 % -- but
  * the 1/4 share took 3.5 % longer with them, profiles/r04_zd_ab_sky_wg.log). */
-template <int kSkyWaves>
+/* GENERAL (round 6): the launch may merge (P.geoColor), hoist, write the accumulator or count segments; the pipelined
+ * faithful whole frames run an instantiation without that code (56 VGPRs and no SGPR spill instead of 59 and 8). */
+template <int kSkyWaves, bool GENERAL>
 __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(RTC_SKY_WAVES))) void rtc_render_sky_rows(
     RenderParams P)
 {
@@ -1338,7 +1340,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
     const bool valid = inFrame && !geo; /* a sky pixel: this kernel renders it */
     /* merged (P.geoColor): the geometry kernel has finished; its pixels' bytes are written here too, so every strip is
      * whole lines.  Their words are requested now and used after the sky loop. */
-    const bool merged = P.geoColor != nullptr; /* (uniform) */
+    const bool merged = GENERAL && P.geoColor != nullptr; /* (uniform) */
     const bool writes = merged ? inFrame : valid;
     const unsigned long long mine = __ballot(writes);
     if (mine == 0ull)
@@ -1366,7 +1368,7 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
     if (valid && P.spp > 0 && P.maxBounce > 0) {
         /* hoisted mode evaluates the primary ray's miss once (a function of the pixel, like its closest hit), faithful
          * mode every sample */
-        if (P.hoist) {
+        if (GENERAL && P.hoist) {
             const V3 l = add(V3{0.f, 0.f, 0.f}, mulv(environment(dir, P.env), V3{1.f, 1.f, 1.f}));
             for (int s = 0; s < P.spp; ++s)
                 acc = add(acc, mul(l, P.invSpp));
@@ -1407,13 +1409,14 @@ __global__ __launch_bounds__(kSkyWaves * 64) __attribute__((amdgpu_waves_per_eu(
         rowp[3 * lane + 1] = c1;
         rowp[3 * lane + 2] = c2;
     }
-    if (valid && P.accum) {
+    if (GENERAL && valid && P.accum) {
         const size_t o = 3 * ((size_t)r * (size_t)P.width + (size_t)x);
         P.accum[o] = acc.x;
         P.accum[o + 1] = acc.y;
         P.accum[o + 2] = acc.z;
     }
-    flush_counters(P, segCalls, segTraced, 0ull, lane);
+    if (GENERAL)
+        flush_counters(P, segCalls, segTraced, 0ull, lane);
 }
 
 /* ---- state-indexed samples (rtc_render_chain, the default for pixels that see geometry) --------------------
@@ -2654,11 +2657,16 @@ extern "C" int rtc_render_rows_async(const RtcDeviceScene *s, const Scene *scene
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky0, os));
             const bool skyWide = pl.smallShare && (size_t)d->width * (size_t)rows > 400000; /* four-wave workgroups */
-            if (skyWide)
-                hipLaunchKernelGGL(rtc_render_sky_rows<4>, dim3((d->width + 63) / 64, (rows + 3) / 4), dim3(256), 0, os,
-                                   P);
+            const bool general = P.geoColor || P.hoist || P.accum || P.segments;
+            const dim3 g4((d->width + 63) / 64, (rows + 3) / 4), g1((d->width + 63) / 64, rows);
+            if (skyWide && general)
+                hipLaunchKernelGGL((rtc_render_sky_rows<4, true>), g4, dim3(256), 0, os, P);
+            else if (skyWide)
+                hipLaunchKernelGGL((rtc_render_sky_rows<4, false>), g4, dim3(256), 0, os, P);
+            else if (general)
+                hipLaunchKernelGGL((rtc_render_sky_rows<1, true>), g1, dim3(64), 0, os, P);
             else
-                hipLaunchKernelGGL(rtc_render_sky_rows<1>, dim3((d->width + 63) / 64, rows), dim3(64), 0, os, P);
+                hipLaunchKernelGGL((rtc_render_sky_rows<1, false>), g1, dim3(64), 0, os, P);
             HIP_TRY(hipGetLastError());
             if (s->timing)
                 HIP_TRY(hipEventRecord(s->evSky1, os));
